@@ -1,0 +1,327 @@
+// cec_kernels.hpp -- CDNA4 (gfx950) HIP kernels for Cocytus' erasure-coding hot path.
+//
+// Every op on the path -- galois_w08_region_multiply, the per-SET
+// diff-update (a2 + a3 = a4), full-stripe encode (a5), the recovery residual (a6)
+// and the leader solve (a7) -- is a GF(2^8) linear combination of byte streams
+// taken at the same arena offset:
+//
+//     out[l][off .. off+len)  (^)=  sum_i  coef[l][i] * in[i][off .. off+len)
+//
+// so one kernel family implements all of them.  A launch walks a work-list of
+// 4 KiB tiles (CEC_UNIT_SIZE, /root/reference/const.h:26) built from the batch's
+// extents; each tile carries a pattern index that selects the inputs, outputs and
+// coefficients (per source shard for diff-update, per erasure mask for decode).
+//
+// Hardware mapping (MI355X):
+//   * 256-thread workgroups, one 16-byte chunk per lane per tile: every stream of
+//     a tile is read with one fully coalesced global_load_dwordx4 per lane
+//     (uniform SGPR base + per-lane VGPR offset);
+//   * tile metadata and coefficient tables are wave-uniform and live in SGPRs
+//     (constant-address-space loads -> s_load);
+//   * GF multiply by a uniform coefficient c on 4 packed bytes:
+//       PERM engine: c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6], three v_perm_b32
+//                    byte lookups per dword (tables are 8 bytes: two SGPRs);
+//       LDS engine : 256-entry log / antilog tables staged in LDS,
+//                    exp[log x + log c] with a zero sentinel (the north-star form);
+//     no MFMA: this is byte-field arithmetic, HBM-bound.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "gf256.hpp"
+
+namespace cec {
+
+constexpr int kTile = 4096;      // bytes per tile = kBlock lanes x 16 B
+constexpr int kBlock = 256;
+constexpr int kMaxStreams = 48;  // 16 data + 8 parity + 16 recovered + staging/diff ...
+constexpr int kPatN = 16;        // inputs per pattern (k <= CEC_MAX_K)
+constexpr int kPatL = 4;         // outputs per launch pattern (host splits more)
+
+enum : int32_t { kModeWrite = 0, kModeXor = 1 };
+
+// One linear combination.  Lives in device memory and is read with scalar loads,
+// so every field is 32-bit (gfx9 scalar loads are dword-granular).
+struct alignas(16) Pattern {
+    int32_t n_in;
+    int32_t n_out;
+    int32_t in_stream[kPatN];
+    int32_t in_src[kPatN];        // 1: address with extent.src_off, 0: with extent.off
+    int32_t out_stream[kPatL];
+    int32_t out_src[kPatL];
+    int32_t out_mode[kPatL];      // kModeWrite / kModeXor
+    int32_t pad[2];
+    int32_t coef[kPatL][kPatN];
+    uint32_t tab[kPatL][kPatN][5];  // PERM: PermTab; LDS: tab[..][0] = log(coef)
+};
+
+struct Extent {  // == cec_extent
+    uint64_t off;
+    uint64_t src_off;
+    uint32_t len;
+    uint32_t pattern;
+};
+
+struct TileEnt {  // one 4 KiB tile of the work-list
+    uint32_t ext;    // extent index
+    uint32_t off;    // byte offset inside the extent (multiple of kTile)
+};
+
+struct CombineArgs {
+    uint8_t *base[kMaxStreams];
+    const Extent *extents;   // NULL: one implicit extent {0, 0, implicit_len, 0}
+    const TileEnt *tiles;
+    const Pattern *patterns;
+    uint64_t implicit_len;
+    uint32_t n_tiles;
+    uint32_t pad;
+};
+
+#define CEC_CONST __attribute__((address_space(4)))
+#define CEC_GLOBAL __attribute__((address_space(1)))
+
+// Read-only kernel inputs are re-addressed in the constant address space so that
+// wave-uniform loads of them become scalar (s_load) loads.
+template <class T>
+__device__ inline const CEC_CONST T *as_const(const T *p) {
+    return (const CEC_CONST T *)(uintptr_t)p;
+}
+
+// Arena bytes: global address space, so a uniform base + per-lane offset becomes
+// global_load_dwordx4 v, v_off, s[base] (no flat addressing, no 64-bit VGPR math).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline uint4 ld16(const uint8_t *base, uint32_t off) {
+    const u32x4 v = *(const CEC_GLOBAL u32x4 *)((uintptr_t)base + off);
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ inline void st16(uint8_t *base, uint32_t off, const uint4 &v) {
+    u32x4 w;
+    w.x = v.x;
+    w.y = v.y;
+    w.z = v.z;
+    w.w = v.w;
+    *(CEC_GLOBAL u32x4 *)((uintptr_t)base + off) = w;
+}
+__device__ inline uint32_t ld8(const uint8_t *base, uint32_t off) {
+    return *(const CEC_GLOBAL uint8_t *)((uintptr_t)base + off);
+}
+__device__ inline void st8(uint8_t *base, uint32_t off, uint32_t v) {
+    *(CEC_GLOBAL uint8_t *)((uintptr_t)base + off) = static_cast<uint8_t>(v);
+}
+
+// ---------------------------------------------------------------- engines
+struct PermEngine {
+    static constexpr int kLdsWords = 1;
+    struct Sel {
+        uint32_t s0, s1, s2;
+    };
+    __device__ static void setup(uint32_t *) {}
+    __device__ static inline Sel sel(uint32_t x, const uint32_t *) {
+        return Sel{x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
+    }
+    __device__ static inline uint32_t mul(const Sel &s, const CEC_CONST uint32_t *t,
+                                          const uint32_t *) {
+        const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], s.s0);
+        const uint32_t b = __builtin_amdgcn_perm(t[3], t[2], s.s1);
+        const uint32_t c = __builtin_amdgcn_perm(t[4], t[4], s.s2);
+        return a ^ b ^ c;
+    }
+};
+
+// LDS layout (uint32 words): [0, 128) log as uint16[256] (log 0 -> 512 sentinel);
+// [128, 384) antilog as uint8[1024]: exp[i] = 2^(i mod 255) for i < 510, 0 above.
+struct LdsEngine {
+    static constexpr int kLdsWords = 384;
+    struct Sel {
+        uint32_t l01, l23;  // log of the 4 bytes, 16 bits each
+    };
+    __device__ static void setup(uint32_t *lds) {
+        uint16_t *lg = reinterpret_cast<uint16_t *>(lds);
+        uint8_t *ex = reinterpret_cast<uint8_t *>(lds + 128);
+        for (int i = threadIdx.x; i < 256; i += blockDim.x)
+            lg[i] = i == 0 ? 512 : static_cast<uint16_t>(kGf.log[i]);
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x)
+            ex[i] = i < 510 ? kGf.exp[i] : 0;
+        __syncthreads();
+    }
+    __device__ static inline Sel sel(uint32_t x, const uint32_t *lds) {
+        const uint16_t *lg = reinterpret_cast<const uint16_t *>(lds);
+        const uint32_t a = lg[x & 0xFF], b = lg[(x >> 8) & 0xFF];
+        const uint32_t c = lg[(x >> 16) & 0xFF], d = lg[x >> 24];
+        return Sel{a | (b << 16), c | (d << 16)};
+    }
+    __device__ static inline uint32_t mul(const Sel &s, const CEC_CONST uint32_t *t,
+                                          const uint32_t *lds) {
+        const uint8_t *ex = reinterpret_cast<const uint8_t *>(lds + 128);
+        const uint32_t lc = t[0];
+        const uint32_t r0 = ex[(s.l01 & 0xFFFF) + lc];
+        const uint32_t r1 = ex[(s.l01 >> 16) + lc];
+        const uint32_t r2 = ex[(s.l23 & 0xFFFF) + lc];
+        const uint32_t r3 = ex[(s.l23 >> 16) + lc];
+        return r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
+    }
+};
+
+// ---------------------------------------------------------------- helpers
+struct TileRef {
+    uint64_t off, src_off;
+    uint32_t len;  // bytes of this tile, 1..kTile
+    uint32_t pattern;
+};
+
+__device__ inline TileRef load_tile(const CombineArgs &a, uint32_t t) {
+    TileRef r;
+    if (a.tiles == nullptr) {
+        const uint64_t o = static_cast<uint64_t>(t) * kTile;
+        const uint64_t rem = a.implicit_len - o;
+        r.off = o;
+        r.src_off = o;
+        r.len = rem < kTile ? static_cast<uint32_t>(rem) : kTile;
+        r.pattern = 0;
+    } else {
+        const CEC_CONST TileEnt *tl = as_const(a.tiles);
+        const uint32_t e = tl[t].ext, to = tl[t].off;
+        const CEC_CONST Extent *ex = as_const(a.extents) + e;
+        r.off = ex->off + to;
+        r.src_off = ex->src_off + to;
+        const uint32_t rem = ex->len - to;
+        r.len = rem < kTile ? rem : kTile;
+        r.pattern = ex->pattern;
+    }
+    return r;
+}
+
+// Byte-granular body for ragged tails and misaligned tiles: bytes b of the tile,
+// b = first, first + step, ... < len.
+template <int NT, int LT, class Eng>
+__device__ inline void combine_bytes(const CEC_CONST Pattern *P, const uint8_t *const *in,
+                                           uint8_t *const *out, int n_in, int n_out,
+                                           uint32_t first, uint32_t step, uint32_t len,
+                                           const uint32_t *lds) {
+    for (uint32_t b = first; b < len; b += step) {
+        uint32_t acc[LT];
+#pragma unroll
+        for (int l = 0; l < LT; ++l)
+            acc[l] = (l < n_out && P->out_mode[l] == kModeXor) ? ld8(out[l], b) : 0u;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            if (i >= n_in) continue;
+            const uint32_t xb = ld8(in[i], b);
+            const typename Eng::Sel s = Eng::sel(xb, lds);
+#pragma unroll
+            for (int l = 0; l < LT; ++l) {
+                if (l >= n_out) continue;
+                const int c = P->coef[l][i];
+                if (c == 0) continue;
+                acc[l] ^= (c == 1) ? xb : (Eng::mul(s, P->tab[l][i], lds) & 0xFFu);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < LT; ++l)
+            if (l < n_out) st8(out[l], b, acc[l]);
+    }
+}
+
+// ---------------------------------------------------------------- the kernel
+// NT / LT: input / output counts.  kExact: the patterns have exactly NT inputs and
+// LT outputs (the hot shapes: straight-line loads, no guards); otherwise NT / LT
+// are capacities and the pattern's n_in / n_out are wave-uniform runtime counts.
+// kAcc: which outputs are read-modify-write (XOR-accumulate):
+//   0 none, 1 all, 2 all but the last (diff-update + install), 3 per pattern.
+enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
+
+template <int NT, int LT, class Eng, int kAcc, bool kExact>
+__global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
+    __shared__ uint32_t lds[Eng::kLdsWords];
+    Eng::setup(lds);
+    const uint32_t lane = threadIdx.x;
+
+    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x) {
+        const TileRef tr = load_tile(a, t);
+        const CEC_CONST Pattern *P = as_const(a.patterns) + tr.pattern;
+        const int n_in = kExact ? NT : P->n_in;
+        const int n_out = kExact ? LT : P->n_out;
+        if (!kExact && n_out == 0) continue;
+        auto is_acc = [&](int l) -> bool {
+            if constexpr (kAcc == kAccNone) return false;
+            else if constexpr (kAcc == kAccAll) return true;
+            else if constexpr (kAcc == kAccAllButLast) return l < LT - 1;
+            else return P->out_mode[l] == kModeXor;
+        };
+
+        const uint8_t *in[NT];
+        uint8_t *out[LT];
+        uint64_t mis = 0;
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            in[i] = nullptr;
+            if (i < n_in) {
+                in[i] = a.base[P->in_stream[i]] + (P->in_src[i] ? tr.src_off : tr.off);
+                mis |= reinterpret_cast<uint64_t>(in[i]);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < LT; ++l) {
+            out[l] = nullptr;
+            if (l < n_out) {
+                out[l] = a.base[P->out_stream[l]] + (P->out_src[l] ? tr.src_off : tr.off);
+                mis |= reinterpret_cast<uint64_t>(out[l]);
+            }
+        }
+
+        if ((mis & 15) != 0) {
+            // misaligned tile (arbitrary device pointers): byte path, coalesced bytes
+            combine_bytes<NT, LT, Eng>(P, in, out, n_in, n_out, lane, kBlock, tr.len, lds);
+            continue;
+        }
+        const uint32_t pos = lane * 16;
+        if (pos + 16 > tr.len) {
+            // ragged tail of the value (len = vlen + 2 is rarely a multiple of 16)
+            if (pos < tr.len) combine_bytes<NT, LT, Eng>(P, in, out, n_in, n_out, pos, 1, tr.len, lds);
+            continue;
+        }
+        uint4 x[NT];
+        uint4 acc[LT];
+#pragma unroll
+        for (int i = 0; i < NT; ++i)
+            if (i < n_in) x[i] = ld16(in[i], pos);
+#pragma unroll
+        for (int l = 0; l < LT; ++l) {
+            acc[l] = make_uint4(0, 0, 0, 0);
+            if (l < n_out && is_acc(l)) acc[l] = ld16(out[l], pos);
+        }
+#pragma unroll
+        for (int i = 0; i < NT; ++i) {
+            if (i >= n_in) continue;
+            const uint32_t xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+            typename Eng::Sel s[4];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) s[w] = Eng::sel(xv[w], lds);
+#pragma unroll
+            for (int l = 0; l < LT; ++l) {
+                if (l >= n_out) continue;
+                const int c = P->coef[l][i];
+                if (c == 0) continue;
+                if (c == 1) {
+                    acc[l].x ^= xv[0];
+                    acc[l].y ^= xv[1];
+                    acc[l].z ^= xv[2];
+                    acc[l].w ^= xv[3];
+                } else {
+                    const CEC_CONST uint32_t *tb = P->tab[l][i];
+                    acc[l].x ^= Eng::mul(s[0], tb, lds);
+                    acc[l].y ^= Eng::mul(s[1], tb, lds);
+                    acc[l].z ^= Eng::mul(s[2], tb, lds);
+                    acc[l].w ^= Eng::mul(s[3], tb, lds);
+                }
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < LT; ++l)
+            if (l < n_out) st16(out[l], pos, acc[l]);
+    }
+}
+
+}  // namespace cec

@@ -1,0 +1,933 @@
+// cec_runtime.hip -- libcocytus_ec.so: the C-ABI of the MI355X erasure-coding path.
+//
+// Exports (a) the three Jerasure 2.x symbols Cocytus links:
+//   galois_w08_region_multiply             (memcached.c:2681,5611,7764,7918; recovery.c:91,123)
+//   reed_sol_big_vandermonde_distribution_matrix   (memcached.c:6845)
+//   jerasure_invert_matrix                 (memcached.c:7907)
+// plus a few same-header helpers, and (b) the batched device API of cocytus_ec.h.
+// Every byte of region arithmetic runs in the HIP kernels of cec_kernels.hpp; the
+// host side only builds coefficient tables, tile work-lists and launches.  There is
+// no CPU fallback: without a gfx950 device the batched API returns CEC_ENODEV and
+// the void Jerasure entry point aborts with a message.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/cocytus_ec.h"
+#include "../../include/galois.h"
+#include "../../include/jerasure.h"
+#include "../../include/reed_sol.h"
+#include "cec_kernels.hpp"
+#include "gf256.hpp"
+
+#define CEC_API extern "C" __attribute__((visibility("default")))
+
+using namespace cec;
+
+static_assert(sizeof(Extent) == sizeof(cec_extent), "extent layout");
+static_assert(CEC_MAX_K <= kPatN, "k capacity");
+
+// ============================================================== errors
+static thread_local char g_err[512] = "";
+
+static int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof(g_err), fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return fail(CEC_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),   \
+                        __FILE__, __LINE__);                                               \
+    } while (0)
+
+[[noreturn]] static void die(const char *what) {
+    fprintf(stderr, "libcocytus_ec: fatal: %s\n", what);
+    fflush(stderr);
+    abort();
+}
+
+// ============================================================== device state
+struct DevInfo {
+    std::once_flag once;
+    int status = CEC_ENODEV;
+    int cus = 256;
+    char msg[256] = "";
+};
+static DevInfo g_dev[64];
+static std::atomic<int> g_engine{CEC_ENGINE_PERM};
+
+static int current_device(int *dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        (void)hipGetLastError();
+        return fail(CEC_ENODEV, "no HIP device visible (libcocytus_ec has no CPU fallback)");
+    }
+    HIP_TRY(hipGetDevice(dev));
+    if (*dev < 0 || *dev >= 64) return fail(CEC_ENODEV, "device ordinal %d out of range", *dev);
+    DevInfo &d = g_dev[*dev];
+    std::call_once(d.once, [&] {
+        hipDeviceProp_t p;
+        if (hipGetDeviceProperties(&p, *dev) != hipSuccess) {
+            snprintf(d.msg, sizeof d.msg, "hipGetDeviceProperties(%d) failed", *dev);
+            return;
+        }
+        if (strncmp(p.gcnArchName, "gfx950", 6) != 0) {
+            snprintf(d.msg, sizeof d.msg, "device %d is %s, libcocytus_ec is built for gfx950",
+                     *dev, p.gcnArchName);
+            return;
+        }
+        d.cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+        d.status = CEC_OK;
+    });
+    if (d.status != CEC_OK) return fail(d.status, "%s", d.msg);
+    return CEC_OK;
+}
+
+// ============================================================== pattern cache
+// Coefficient tables are small and reused for every launch of an op with the same
+// code; they are uploaded once per (device, content) and kept for the process.
+struct PatternCache {
+    std::mutex mu;
+    std::map<std::string, Pattern *> map;
+};
+static PatternCache g_pcache[64];
+
+static int upload_patterns(int dev, const std::vector<Pattern> &pats, const Pattern **out) {
+    std::string key(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
+    PatternCache &c = g_pcache[dev];
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto it = c.map.find(key);
+    if (it != c.map.end()) {
+        *out = it->second;
+        return CEC_OK;
+    }
+    Pattern *d = nullptr;
+    if (hipMalloc(&d, key.size()) != hipSuccess)
+        return fail(CEC_ENOMEM, "hipMalloc(%zu) for coefficient tables failed", key.size());
+    HIP_TRY(hipMemcpy(d, key.data(), key.size(), hipMemcpyHostToDevice));
+    c.map.emplace(std::move(key), d);
+    *out = d;
+    return CEC_OK;
+}
+
+static Pattern blank_pattern() {
+    Pattern p;
+    memset(&p, 0, sizeof p);
+    return p;
+}
+
+static void set_coef(Pattern &p, int l, int i, int c, int engine) {
+    c &= 0xFF;
+    p.coef[l][i] = static_cast<uint8_t>(c);
+    if (engine == CEC_ENGINE_LDS) {
+        p.tab[l][i][0] = c ? static_cast<uint32_t>(kGf.log[c]) : 0u;
+    } else {
+        const PermTab t = make_perm_tab(c);
+        for (int w = 0; w < 5; ++w) p.tab[l][i][w] = t.w[w];
+    }
+}
+
+// ============================================================== launch
+template <int NT, int LT, class Eng, int kAcc, bool kExact>
+static void launch_k(const CombineArgs &a, int grid, hipStream_t s) {
+    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid), dim3(kBlock), 0,
+                       s, a);
+}
+
+// Exact-shape kernels for the hot ops: encode / decode / residual / solve (no RMW,
+// up to 8 inputs x 4 outputs), parity apply and region multiply-XOR (1 x 1 RMW),
+// diff-update (2 inputs, M parity RMW outputs, optionally + install).
+template <class Eng>
+static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, hipStream_t s) {
+#define CEC_X(N, L, A)                                           \
+    if (n == N && l == L && acc == A) {                          \
+        launch_k<N, L, Eng, A, true>(a, grid, s);                \
+        return true;                                             \
+    }
+#define CEC_XL(N) CEC_X(N, 1, kAccNone) CEC_X(N, 2, kAccNone) CEC_X(N, 3, kAccNone) CEC_X(N, 4, kAccNone)
+    CEC_XL(1) CEC_XL(2) CEC_XL(3) CEC_XL(4) CEC_XL(5) CEC_XL(6) CEC_XL(7) CEC_XL(8)
+    CEC_X(1, 1, kAccAll) CEC_X(2, 1, kAccAll) CEC_X(2, 2, kAccAll) CEC_X(2, 3, kAccAll)
+    CEC_X(2, 4, kAccAll) CEC_X(2, 2, kAccAllButLast) CEC_X(2, 3, kAccAllButLast)
+    CEC_X(2, 4, kAccAllButLast)
+#undef CEC_XL
+#undef CEC_X
+    return false;
+}
+
+// Capacity kernels for every other shape (guarded, per-pattern counts and modes).
+template <class Eng>
+static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, hipStream_t s) {
+#define CEC_G(NT)                                                                    \
+    if (lt <= 1) launch_k<NT, 1, Eng, kAccRuntime, false>(a, grid, s);              \
+    else if (lt <= 2) launch_k<NT, 2, Eng, kAccRuntime, false>(a, grid, s);         \
+    else launch_k<NT, 4, Eng, kAccRuntime, false>(a, grid, s);
+    if (nt <= 2) { CEC_G(2) }
+    else if (nt <= 4) { CEC_G(4) }
+    else if (nt <= 8) { CEC_G(8) }
+    else { CEC_G(16) }
+#undef CEC_G
+}
+
+// Shape class of a pattern set: exact (n_in, n_out, acc) if all patterns agree.
+static bool exact_shape(const std::vector<Pattern> &pats, int *n, int *l, int *acc) {
+    const Pattern &p0 = pats[0];
+    for (const Pattern &p : pats) {
+        if (p.n_in != p0.n_in || p.n_out != p0.n_out) return false;
+        for (int o = 0; o < p.n_out; ++o)
+            if (p.out_mode[o] != p0.out_mode[o]) return false;
+    }
+    int nx = 0;
+    for (int o = 0; o < p0.n_out; ++o) nx += p0.out_mode[o] == kModeXor;
+    if (nx == 0) *acc = kAccNone;
+    else if (nx == p0.n_out) *acc = kAccAll;
+    else if (nx == p0.n_out - 1 && p0.out_mode[p0.n_out - 1] == kModeWrite) *acc = kAccAllButLast;
+    else return false;
+    *n = p0.n_in;
+    *l = p0.n_out;
+    return true;
+}
+
+struct Streams {
+    uint8_t *base[kMaxStreams] = {};
+};
+
+// One launch over a tile source (plan or implicit region) with a pattern set.
+static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
+                       const cec_plan *plan, uint64_t implicit_len, hipStream_t stream);
+
+// ============================================================== plans
+struct cec_plan {
+    int device = -1;
+    int n_ext = 0;
+    int64_t n_tiles = 0;
+    uint64_t total = 0;
+    bool overlap = false;
+    Extent *d_ext = nullptr;
+    TileEnt *d_tiles = nullptr;
+    std::vector<cec_extent> h_ext;  // kept alive for the async upload
+    std::vector<TileEnt> h_tiles;
+};
+
+CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *stream) {
+    if (!out || n < 0 || (n > 0 && !ext)) return fail(CEC_EINVAL, "cec_plan_create: bad args");
+    *out = nullptr;
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    cec_plan *p = new (std::nothrow) cec_plan;
+    if (!p) return fail(CEC_ENOMEM, "cec_plan_create: host allocation");
+    p->device = dev;
+    p->n_ext = n;
+    p->h_ext.assign(ext, ext + n);
+    for (int e = 0; e < n; ++e) {
+        const uint32_t len = ext[e].len;
+        p->total += len;
+        for (uint32_t o = 0; o < len; o += kTile) p->h_tiles.push_back(TileEnt{static_cast<uint32_t>(e), o});
+    }
+    if (p->h_tiles.size() > 0xFFFFFFFFull) {
+        delete p;
+        return fail(CEC_EINVAL, "cec_plan_create: more than 2^32 tiles");
+    }
+    p->n_tiles = static_cast<int64_t>(p->h_tiles.size());
+    {   // overlap of [off, off+len) among non-empty extents
+        std::vector<std::pair<uint64_t, uint64_t>> r;
+        r.reserve(n);
+        for (int e = 0; e < n; ++e)
+            if (ext[e].len) r.emplace_back(ext[e].off, ext[e].off + ext[e].len);
+        std::sort(r.begin(), r.end());
+        for (size_t i = 1; i < r.size(); ++i)
+            if (r[i].first < r[i - 1].second) { p->overlap = true; break; }
+    }
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (n > 0) {
+        if (hipMalloc(&p->d_ext, sizeof(Extent) * n) != hipSuccess) {
+            delete p;
+            return fail(CEC_ENOMEM, "cec_plan_create: hipMalloc extents");
+        }
+        HIP_TRY(hipMemcpyAsync(p->d_ext, p->h_ext.data(), sizeof(Extent) * n,
+                               hipMemcpyHostToDevice, s));
+    }
+    if (p->n_tiles > 0) {
+        if (hipMalloc(&p->d_tiles, sizeof(TileEnt) * p->n_tiles) != hipSuccess) {
+            (void)hipFree(p->d_ext);
+            delete p;
+            return fail(CEC_ENOMEM, "cec_plan_create: hipMalloc tiles");
+        }
+        HIP_TRY(hipMemcpyAsync(p->d_tiles, p->h_tiles.data(), sizeof(TileEnt) * p->n_tiles,
+                               hipMemcpyHostToDevice, s));
+    }
+    *out = p;
+    return CEC_OK;
+}
+
+CEC_API int cec_plan_destroy(cec_plan *p) {
+    if (!p) return CEC_OK;
+    int rc = CEC_OK;
+    if (hipDeviceSynchronize() != hipSuccess) rc = fail(CEC_EHIP, "hipDeviceSynchronize");
+    if (p->d_ext) (void)hipFree(p->d_ext);
+    if (p->d_tiles) (void)hipFree(p->d_tiles);
+    delete p;
+    return rc;
+}
+
+CEC_API int cec_plan_num_extents(const cec_plan *p) { return p ? p->n_ext : 0; }
+CEC_API int64_t cec_plan_num_tiles(const cec_plan *p) { return p ? p->n_tiles : 0; }
+CEC_API uint64_t cec_plan_total_bytes(const cec_plan *p) { return p ? p->total : 0; }
+
+static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
+                       const cec_plan *plan, uint64_t implicit_len, hipStream_t stream) {
+    CombineArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
+    uint64_t n_tiles;
+    if (plan) {
+        if (plan->device != dev)
+            return fail(CEC_EINVAL, "plan built on device %d used on device %d", plan->device, dev);
+        a.extents = plan->d_ext;
+        a.tiles = plan->d_tiles;
+        n_tiles = static_cast<uint64_t>(plan->n_tiles);
+    } else {
+        a.implicit_len = implicit_len;
+        n_tiles = (implicit_len + kTile - 1) / kTile;
+        if (n_tiles > 0xFFFFFFFFull) return fail(CEC_EINVAL, "region too large");
+    }
+    if (n_tiles == 0 || pats.empty()) return CEC_OK;
+    int nt = 1, lt = 0;
+    for (const Pattern &p : pats) {
+        nt = std::max(nt, p.n_in);
+        lt = std::max(lt, p.n_out);
+    }
+    if (lt == 0) return CEC_OK;
+    const Pattern *dp = nullptr;
+    if (int r = upload_patterns(dev, pats, &dp)) return r;
+    a.patterns = dp;
+    a.n_tiles = static_cast<uint32_t>(n_tiles);
+    const uint64_t max_grid = static_cast<uint64_t>(g_dev[dev].cus) * 8;
+    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles, max_grid));
+    int en, el, eacc;
+    const bool lds = g_engine.load() == CEC_ENGINE_LDS;
+    const bool exact = exact_shape(pats, &en, &el, &eacc) &&
+                       (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, stream)
+                            : launch_exact<PermEngine>(en, el, eacc, a, grid, stream));
+    if (!exact) {
+        if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, stream);
+        else launch_generic<PermEngine>(nt, lt, a, grid, stream);
+    }
+    HIP_TRY(hipGetLastError());
+    return CEC_OK;
+}
+
+// Logical pattern with arbitrarily many outputs, before splitting.
+struct Combo {
+    int n_in = 0;
+    uint8_t in_stream[kPatN] = {};
+    uint8_t in_src[kPatN] = {};
+    struct Out {
+        uint8_t stream, src, mode;
+        int coef[kPatN];
+    };
+    std::vector<Out> outs;  // install output (if any) is last
+};
+
+static int run_combos(int dev, const Streams &st, const std::vector<Combo> &combos,
+                      const cec_plan *plan, uint64_t implicit_len, hipStream_t stream) {
+    size_t max_out = 0;
+    for (const Combo &c : combos) max_out = std::max(max_out, c.outs.size());
+    const int engine = g_engine.load();
+    const size_t groups = (max_out + kPatL - 1) / kPatL;
+    for (size_t g = 0; g < groups; ++g) {
+        std::vector<Pattern> pats;
+        pats.reserve(combos.size());
+        for (const Combo &c : combos) {
+            Pattern p = blank_pattern();
+            p.n_in = c.n_in;
+            for (int i = 0; i < c.n_in; ++i) {
+                p.in_stream[i] = c.in_stream[i];
+                p.in_src[i] = c.in_src[i];
+            }
+            // Launch g carries outputs [4g, 4g+4); an install output is last in
+            // `outs`, so it runs in the final launch after every group read old bytes.
+            const size_t n = c.outs.size();
+            const size_t lo = g * kPatL, hi = std::min(n, lo + kPatL);
+            int no = 0;
+            for (size_t o = lo; o < hi; ++o, ++no) {
+                const Combo::Out &q = c.outs[o];
+                p.out_stream[no] = q.stream;
+                p.out_src[no] = q.src;
+                p.out_mode[no] = q.mode;
+                for (int i = 0; i < c.n_in; ++i) set_coef(p, no, i, q.coef[i], engine);
+            }
+            p.n_out = no;
+            pats.push_back(p);
+        }
+        if (int r = run_combine(dev, st, pats, plan, implicit_len, stream)) return r;
+    }
+    return CEC_OK;
+}
+
+static int check_code(int k, int m, const int *matrix) {
+    if (k < 1 || k > CEC_MAX_K || m < 1 || m > CEC_MAX_M || k + m > 32)
+        return fail(CEC_EINVAL, "unsupported code k=%d m=%d (1<=k<=%d, 1<=m<=%d, k+m<=32)", k, m,
+                    CEC_MAX_K, CEC_MAX_M);
+    if (!matrix) return fail(CEC_EINVAL, "matrix is NULL");
+    for (int i = 0; i < (k + m) * k; ++i)
+        if (matrix[i] < 0 || matrix[i] > 255)
+            return fail(CEC_EINVAL, "matrix entry %d = %d outside GF(2^8)", i, matrix[i]);
+    return CEC_OK;
+}
+
+#define MATRIX(x, y) matrix[(x) * k + (y)]
+
+// ============================================================== runtime API
+CEC_API const char *cec_version(void) { return "cocytus_ec 0.1 (gfx950)"; }
+CEC_API const char *cec_last_error(void) { return g_err; }
+CEC_API int cec_device_check(void) {
+    int dev;
+    return current_device(&dev);
+}
+CEC_API int cec_set_engine(cec_engine e) {
+    if (e != CEC_ENGINE_PERM && e != CEC_ENGINE_LDS) return fail(CEC_EINVAL, "bad engine %d", e);
+    g_engine.store(e);
+    return CEC_OK;
+}
+CEC_API cec_engine cec_get_engine(void) { return static_cast<cec_engine>(g_engine.load()); }
+
+// ============================================================== ops
+CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void *dst, int add,
+                                void *stream) {
+    if (!src || multby < 0 || multby > 255) return fail(CEC_EINVAL, "cec_region_multiply: bad args");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    if (nbytes == 0) return CEC_OK;
+    if (!dst) {
+        dst = const_cast<void *>(src);
+        add = 0;
+    }
+    if (add && multby == 0) return CEC_OK;
+    Streams st;
+    st.base[0] = static_cast<uint8_t *>(const_cast<void *>(src));
+    st.base[1] = static_cast<uint8_t *>(dst);
+    Combo c;
+    c.n_in = 1;
+    c.in_stream[0] = 0;
+    Combo::Out o{};
+    o.stream = 1;
+    o.mode = add ? kModeXor : kModeWrite;
+    o.coef[0] = multby;
+    c.outs.push_back(o);
+    return run_combos(dev, st, {c}, nullptr, nbytes, static_cast<hipStream_t>(stream));
+}
+
+static int encode_common(int k, int m, const int *matrix, const uint8_t *const *data,
+                         uint8_t *const *parity, const cec_plan *plan, uint64_t len,
+                         void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (!data || !parity) return fail(CEC_EINVAL, "cec_encode: NULL arena array");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    Streams st;
+    Combo c;
+    c.n_in = k;
+    for (int j = 0; j < k; ++j) {
+        if (!data[j]) return fail(CEC_EINVAL, "cec_encode: data[%d] is NULL", j);
+        st.base[j] = const_cast<uint8_t *>(data[j]);
+        c.in_stream[j] = static_cast<uint8_t>(j);
+    }
+    for (int p = 0; p < m; ++p) {
+        if (!parity[p]) continue;  // a lost parity is simply not produced
+        st.base[k + p] = parity[p];
+        Combo::Out o{};
+        o.stream = static_cast<uint8_t>(k + p);
+        o.mode = kModeWrite;
+        for (int j = 0; j < k; ++j) o.coef[j] = MATRIX(k + p, j);
+        c.outs.push_back(o);
+    }
+    return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream));
+}
+
+CEC_API int cec_encode(int k, int m, const int *matrix, const uint8_t *const *data,
+                       uint8_t *const *parity, const cec_plan *plan, void *stream) {
+    if (!plan) return fail(CEC_EINVAL, "cec_encode: plan is NULL");
+    return encode_common(k, m, matrix, data, parity, plan, 0, stream);
+}
+
+CEC_API int cec_encode_region(int k, int m, const int *matrix, const uint8_t *const *data,
+                              uint8_t *const *parity, size_t len, void *stream) {
+    return encode_common(k, m, matrix, data, parity, nullptr, len, stream);
+}
+
+CEC_API int cec_diff_update(int k, int m, const int *matrix, uint8_t *const *data,
+                            const uint8_t *staging, uint8_t *const *parity, int install,
+                            const cec_plan *plan, void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (!plan || !data || !staging || !parity) return fail(CEC_EINVAL, "cec_diff_update: NULL arg");
+    if (plan->overlap) return fail(CEC_EOVERLAP, "cec_diff_update: plan extents overlap");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    Streams st;
+    for (int j = 0; j < k; ++j) {
+        if (!data[j]) return fail(CEC_EINVAL, "cec_diff_update: data[%d] is NULL", j);
+        st.base[j] = data[j];
+    }
+    for (int p = 0; p < m; ++p) st.base[k + p] = parity[p];
+    st.base[k + m] = const_cast<uint8_t *>(staging);
+    std::vector<Combo> combos(k);
+    for (int j = 0; j < k; ++j) {
+        Combo &c = combos[j];
+        c.n_in = 2;
+        c.in_stream[0] = static_cast<uint8_t>(j);      // old bytes, arena offset
+        c.in_stream[1] = static_cast<uint8_t>(k + m);  // new value, staging offset
+        c.in_src[1] = 1;
+        for (int p = 0; p < m; ++p) {
+            if (!parity[p]) continue;  // lost parity: skipped like memcached.c:2692-2694
+            Combo::Out o{};
+            o.stream = static_cast<uint8_t>(k + p);
+            o.mode = kModeXor;
+            o.coef[0] = o.coef[1] = MATRIX(k + p, j);
+            c.outs.push_back(o);
+        }
+        if (install) {
+            Combo::Out o{};
+            o.stream = static_cast<uint8_t>(j);
+            o.mode = kModeWrite;
+            o.coef[0] = 0;
+            o.coef[1] = 1;
+            c.outs.push_back(o);
+        }
+    }
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+CEC_API int cec_set_diff(int k, const uint8_t *const *data, const uint8_t *staging, uint8_t *diff,
+                         const cec_plan *plan, void *stream) {
+    if (k < 1 || k > CEC_MAX_K || !plan || !data || !staging || !diff)
+        return fail(CEC_EINVAL, "cec_set_diff: bad args");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    Streams st;
+    for (int j = 0; j < k; ++j) {
+        if (!data[j]) return fail(CEC_EINVAL, "cec_set_diff: data[%d] is NULL", j);
+        st.base[j] = const_cast<uint8_t *>(data[j]);
+    }
+    st.base[k] = const_cast<uint8_t *>(staging);
+    st.base[k + 1] = diff;
+    std::vector<Combo> combos(k);
+    for (int j = 0; j < k; ++j) {
+        Combo &c = combos[j];
+        c.n_in = 2;
+        c.in_stream[0] = static_cast<uint8_t>(j);
+        c.in_stream[1] = static_cast<uint8_t>(k);
+        c.in_src[1] = 1;
+        Combo::Out o{};
+        o.stream = static_cast<uint8_t>(k + 1);
+        o.src = 1;
+        o.mode = kModeWrite;
+        o.coef[0] = o.coef[1] = 1;
+        c.outs.push_back(o);
+    }
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+CEC_API int cec_apply_diffs(int k, int m, const int *matrix, int lid_self, const uint8_t *diffs,
+                            uint8_t *parity, const cec_plan *plan, void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (lid_self < k || lid_self >= k + m || !diffs || !parity || !plan)
+        return fail(CEC_EINVAL, "cec_apply_diffs: bad args (lid_self=%d)", lid_self);
+    if (plan->overlap) return fail(CEC_EOVERLAP, "cec_apply_diffs: plan extents overlap");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    Streams st;
+    st.base[0] = const_cast<uint8_t *>(diffs);
+    st.base[1] = parity;
+    std::vector<Combo> combos(k);
+    for (int j = 0; j < k; ++j) {
+        Combo &c = combos[j];
+        c.n_in = 1;
+        c.in_stream[0] = 0;
+        c.in_src[0] = 1;
+        Combo::Out o{};
+        o.stream = 1;
+        o.mode = kModeXor;
+        o.coef[0] = MATRIX(lid_self, j);
+        c.outs.push_back(o);
+    }
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+static int mask_ok(int k, int m, uint32_t mask) {
+    if (k + m < 32 && (mask >> (k + m)) != 0) return 0;
+    return __builtin_popcount(mask) == k;
+}
+
+CEC_API int cec_residual(int k, int m, const int *matrix, int lid_self, uint32_t mask,
+                         const uint8_t *const *arenas, uint8_t *residual, const cec_plan *plan,
+                         void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (lid_self < k || lid_self >= k + m || !arenas || !residual || !plan)
+        return fail(CEC_EINVAL, "cec_residual: bad args");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    Streams st;
+    Combo c;
+    Combo::Out o{};
+    o.stream = static_cast<uint8_t>(k + m);
+    o.mode = kModeWrite;
+    if (!arenas[lid_self]) return fail(CEC_EINVAL, "cec_residual: own parity arena is NULL");
+    st.base[lid_self] = const_cast<uint8_t *>(arenas[lid_self]);
+    c.in_stream[c.n_in] = static_cast<uint8_t>(lid_self);
+    o.coef[c.n_in++] = 1;  // first touch copies the parity unit (recovery.c:79-82)
+    for (int s = 0; s < k; ++s) {
+        if (!(mask & (1u << s))) continue;
+        if (!arenas[s]) return fail(CEC_EINVAL, "cec_residual: arena %d in mask is NULL", s);
+        st.base[s] = const_cast<uint8_t *>(arenas[s]);
+        c.in_stream[c.n_in] = static_cast<uint8_t>(s);
+        o.coef[c.n_in++] = MATRIX(lid_self, s);  // recovery.c:91-93
+    }
+    st.base[k + m] = residual;
+    c.outs.push_back(o);
+    return run_combos(dev, st, {c}, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+// Lost data lids and participating parity lids of a recovery mask, ascending
+// (complete_recovery_bottom_half, memcached.c:7847-7894).
+static int mask_split(int k, int m, uint32_t mask, int *lost, int *pars) {
+    int n = 0, r = 0;
+    for (int j = 0; j < k; ++j)
+        if (!(mask & (1u << j))) lost[n++] = j;
+    for (int p = k; p < k + m; ++p)
+        if (mask & (1u << p)) pars[r++] = p;
+    return n == r ? n : -1;
+}
+
+static int solve_inverse(int k, const int *matrix, int n, const int *lost, const int *pars,
+                         int *inv) {
+    int tmp[CEC_MAX_M * CEC_MAX_M];
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) tmp[r * n + c] = MATRIX(pars[r], lost[c]);
+    return invert_matrix(tmp, inv, n);
+}
+
+CEC_API int cec_solve(int k, int m, const int *matrix, uint32_t mask,
+                      const uint8_t *const *residuals, uint8_t *const *out, const cec_plan *plan,
+                      void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (!mask_ok(k, m, mask) || !residuals || !out || !plan)
+        return fail(CEC_EINVAL, "cec_solve: bad args (mask=0x%x)", mask);
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    int lost[CEC_MAX_K], pars[CEC_MAX_M], inv[CEC_MAX_M * CEC_MAX_M];
+    const int n = mask_split(k, m, mask, lost, pars);
+    if (n < 0) return fail(CEC_EINVAL, "cec_solve: mask 0x%x is not a recovery mask", mask);
+    if (n == 0) return CEC_OK;
+    if (solve_inverse(k, matrix, n, lost, pars, inv))
+        return fail(CEC_ESINGULAR, "cec_solve: singular submatrix for mask 0x%x", mask);
+    Streams st;
+    Combo c;
+    c.n_in = n;
+    for (int r = 0; r < n; ++r) {
+        if (!residuals[pars[r]]) return fail(CEC_EINVAL, "cec_solve: residual %d NULL", pars[r]);
+        st.base[r] = const_cast<uint8_t *>(residuals[pars[r]]);
+        c.in_stream[r] = static_cast<uint8_t>(r);
+    }
+    for (int x = 0; x < n; ++x) {
+        if (!out[lost[x]]) return fail(CEC_EINVAL, "cec_solve: out[%d] NULL", lost[x]);
+        st.base[CEC_MAX_M + x] = out[lost[x]];
+        Combo::Out o{};
+        o.stream = static_cast<uint8_t>(CEC_MAX_M + x);
+        o.mode = kModeWrite;
+        for (int r = 0; r < n; ++r) o.coef[r] = inv[x * n + r];  // memcached.c:7916-7922
+        c.outs.push_back(o);
+    }
+    return run_combos(dev, st, {c}, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, int n_masks,
+                       const uint8_t *const *arenas, uint8_t *const *out, const cec_plan *plan,
+                       void *stream) {
+    if (int r = check_code(k, m, matrix)) return r;
+    if (!masks || n_masks < 1 || !arenas || !out || !plan)
+        return fail(CEC_EINVAL, "cec_decode: bad args");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    for (int e = 0; e < plan->n_ext; ++e)
+        if (plan->h_ext[e].pattern >= static_cast<uint32_t>(n_masks))
+            return fail(CEC_EINVAL, "cec_decode: extent %d names mask %u of %d", e,
+                        plan->h_ext[e].pattern, n_masks);
+    Streams st;
+    for (int lid = 0; lid < k + m; ++lid) st.base[lid] = const_cast<uint8_t *>(arenas[lid]);
+    for (int j = 0; j < k; ++j) st.base[k + m + j] = out[j];
+    std::vector<Combo> combos(n_masks);
+    for (int q = 0; q < n_masks; ++q) {
+        const uint32_t mask = masks[q];
+        if (!mask_ok(k, m, mask)) return fail(CEC_EINVAL, "cec_decode: bad mask 0x%x", mask);
+        int lost[CEC_MAX_K], pars[CEC_MAX_M], inv[CEC_MAX_M * CEC_MAX_M];
+        const int n = mask_split(k, m, mask, lost, pars);
+        if (n < 0) return fail(CEC_EINVAL, "cec_decode: mask 0x%x is not a recovery mask", mask);
+        if (n > 0 && solve_inverse(k, matrix, n, lost, pars, inv))
+            return fail(CEC_ESINGULAR, "cec_decode: singular submatrix for mask 0x%x", mask);
+        Combo &c = combos[q];
+        // inputs: the n participating parities, then the k-n surviving data shards
+        int surv[CEC_MAX_K], ns = 0;
+        for (int j = 0; j < k; ++j)
+            if (mask & (1u << j)) surv[ns++] = j;
+        for (int r = 0; r < n; ++r) c.in_stream[c.n_in++] = static_cast<uint8_t>(pars[r]);
+        for (int s = 0; s < ns; ++s) c.in_stream[c.n_in++] = static_cast<uint8_t>(surv[s]);
+        for (int i = 0; i < c.n_in; ++i)
+            if (!arenas[c.in_stream[i]])
+                return fail(CEC_EINVAL, "cec_decode: arena %d (in mask 0x%x) is NULL",
+                            c.in_stream[i], mask);
+        // D_lost[x] = sum_r inv[x][r] * (P_r ^ sum_s MATRIX(P_r, s) * D_s)
+        for (int x = 0; x < n; ++x) {
+            if (!out[lost[x]]) return fail(CEC_EINVAL, "cec_decode: out[%d] is NULL", lost[x]);
+            Combo::Out o{};
+            o.stream = static_cast<uint8_t>(k + m + lost[x]);
+            o.mode = kModeWrite;
+            for (int r = 0; r < n; ++r) o.coef[r] = inv[x * n + r];
+            for (int s = 0; s < ns; ++s) {
+                int acc = 0;
+                for (int r = 0; r < n; ++r) acc ^= gf_mul(inv[x * n + r], MATRIX(pars[r], surv[s]));
+                o.coef[n + s] = acc;
+            }
+            c.outs.push_back(o);
+        }
+    }
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+}
+
+CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected) {
+    if (k < 1 || m < 1 || k + m > 32 || !connected || leader_lid < 0 || leader_lid >= k + m)
+        return 0;
+    int remaining = k - 1;
+    uint32_t mask = 1u << leader_lid;
+    for (int i = 0; i < k + m && remaining; ++i) {
+        if (i == leader_lid || !connected[i]) continue;
+        mask |= 1u << i;
+        --remaining;
+    }
+    return remaining ? 0u : mask;
+}
+
+// ============================================================== events / streams
+CEC_API int cec_event_create(void **ev) {
+    if (!ev) return fail(CEC_EINVAL, "NULL");
+    hipEvent_t e;
+    HIP_TRY(hipEventCreate(&e));
+    *ev = e;
+    return CEC_OK;
+}
+CEC_API int cec_event_destroy(void *ev) {
+    HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(ev)));
+    return CEC_OK;
+}
+CEC_API int cec_event_record(void *ev, void *stream) {
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+CEC_API int cec_event_elapsed_ms(void *a, void *b, float *ms) {
+    HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(b)));
+    HIP_TRY(hipEventElapsedTime(ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)));
+    return CEC_OK;
+}
+CEC_API int cec_stream_synchronize(void *stream) {
+    HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+// ============================================================== Jerasure drop-in
+CEC_API int galois_single_multiply(int a, int b, int w) {
+    if (w != 8) die("galois_single_multiply: only w = 8 is provided");
+    return gf_mul(a, b);
+}
+CEC_API int galois_single_divide(int a, int b, int w) {
+    if (w != 8) die("galois_single_divide: only w = 8 is provided");
+    if ((b & 0xFF) == 0) return -1;
+    return gf_div(a, b);
+}
+CEC_API int galois_inverse(int x, int w) { return galois_single_divide(1, x, w); }
+
+CEC_API int *reed_sol_extended_vandermonde_matrix(int rows, int cols, int w) {
+    if (w != 8 || rows < 1 || cols < 1 || rows > 256 || cols > 256) return nullptr;
+    int *v = static_cast<int *>(calloc(static_cast<size_t>(rows) * cols, sizeof(int)));
+    if (!v) return nullptr;
+    v[0] = 1;
+    if (rows == 1) return v;
+    v[rows * cols - 1] = 1;
+    for (int r = 1; r + 1 < rows; ++r)
+        for (int c = 0, x = 1; c < cols; ++c, x = gf_mul(x, r)) v[r * cols + c] = x;
+    return v;
+}
+
+CEC_API int *reed_sol_big_vandermonde_distribution_matrix(int rows, int cols, int w) {
+    if (cols >= rows) return nullptr;
+    int *m = reed_sol_extended_vandermonde_matrix(rows, cols, w);
+    if (!m) return nullptr;
+    auto at = [&](int r, int c) -> int & { return m[r * cols + c]; };
+    for (int i = 1; i < cols; ++i) {  // column-reduce the top block to identity
+        int r = i;
+        while (r < rows && at(r, i) == 0) ++r;
+        if (r == rows) { free(m); return nullptr; }
+        if (r != i)
+            for (int c = 0; c < cols; ++c) std::swap(at(r, c), at(i, c));
+        if (at(i, i) != 1) {
+            const int s = gf_inv(at(i, i));
+            for (int q = 0; q < rows; ++q) at(q, i) = gf_mul(s, at(q, i));
+        }
+        for (int c = 0; c < cols; ++c) {
+            const int e = at(i, c);
+            if (c != i && e)
+                for (int q = 0; q < rows; ++q) at(q, c) ^= gf_mul(e, at(q, i));
+        }
+    }
+    for (int c = 0; c < cols; ++c) {  // first parity row -> all ones
+        const int e = at(cols, c);
+        if (e != 1) {
+            const int s = gf_inv(e);
+            for (int q = cols; q < rows; ++q) at(q, c) = gf_mul(s, at(q, c));
+        }
+    }
+    for (int q = cols + 1; q < rows; ++q) {  // first column of later parity rows -> one
+        const int e = at(q, 0);
+        if (e != 1) {
+            const int s = gf_inv(e);
+            for (int c = 0; c < cols; ++c) at(q, c) = gf_mul(at(q, c), s);
+        }
+    }
+    return m;
+}
+
+CEC_API int jerasure_invert_matrix(int *mat, int *inv, int rows, int w) {
+    if (w != 8) {
+        fprintf(stderr, "libcocytus_ec: jerasure_invert_matrix: only w = 8 is provided\n");
+        return -1;
+    }
+    if (!mat || !inv || rows < 1) return -1;
+    return invert_matrix(mat, inv, rows);
+}
+
+CEC_API int *jerasure_matrix_multiply(int *m1, int *m2, int r1, int c1, int r2, int c2, int w) {
+    if (w != 8 || c1 != r2 || r1 < 1 || c2 < 1) return nullptr;
+    int *p = static_cast<int *>(calloc(static_cast<size_t>(r1) * c2, sizeof(int)));
+    if (!p) return nullptr;
+    for (int i = 0; i < r1; ++i)
+        for (int j = 0; j < c2; ++j) {
+            int acc = 0;
+            for (int x = 0; x < c1; ++x) acc ^= gf_mul(m1[i * c1 + x], m2[x * c2 + j]);
+            p[i * c2 + j] = acc;
+        }
+    return p;
+}
+
+// Per-thread context of the synchronous drop-in: a stream and device staging.
+namespace {
+struct DropInCtx {
+    int device = -1;
+    hipStream_t stream = nullptr;
+    uint8_t *dsrc = nullptr, *ddst = nullptr;
+    size_t cap = 0;
+    ~DropInCtx() {
+        if (stream) {
+            (void)hipStreamSynchronize(stream);
+            (void)hipStreamDestroy(stream);
+        }
+        if (dsrc) (void)hipFree(dsrc);
+        if (ddst) (void)hipFree(ddst);
+    }
+};
+thread_local DropInCtx t_ctx;
+constexpr size_t kStageChunk = size_t(64) << 20;
+
+// Device-usable address for p, or NULL if p is pageable host memory.
+void *device_view(void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged ||
+        at.type == hipMemoryTypeHost)
+        return at.devicePointer;
+    return nullptr;
+}
+}  // namespace
+
+#define DROPIN_CHECK(expr)                                                                  \
+    do {                                                                                    \
+        int rc_ = (expr);                                                                   \
+        if (rc_ != CEC_OK) {                                                                \
+            char b_[640];                                                                   \
+            snprintf(b_, sizeof b_, "galois_w08_region_multiply: %s", g_err);              \
+            die(b_);                                                                        \
+        }                                                                                   \
+    } while (0)
+#define DROPIN_HIP(expr)                                                                    \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) {                                                             \
+            char b_[256];                                                                   \
+            snprintf(b_, sizeof b_, "galois_w08_region_multiply: %s: %s", #expr,           \
+                     hipGetErrorString(e_));                                                \
+            die(b_);                                                                        \
+        }                                                                                   \
+    } while (0)
+
+CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, char *r2, int add) {
+    if (multby < 0 || multby > 255) die("galois_w08_region_multiply: multby outside [0, 255]");
+    if (nbytes <= 0) return;
+    if (!region) die("galois_w08_region_multiply: region is NULL");
+    if (r2 && add && multby == 0) return;
+    int dev;
+    DROPIN_CHECK(current_device(&dev));
+    DropInCtx &c = t_ctx;
+    if (c.device != dev) {
+        if (c.stream) DROPIN_HIP(hipStreamDestroy(c.stream));
+        c.stream = nullptr;
+        if (c.dsrc) DROPIN_HIP(hipFree(c.dsrc));
+        if (c.ddst) DROPIN_HIP(hipFree(c.ddst));
+        c.dsrc = c.ddst = nullptr;
+        c.cap = 0;
+        DROPIN_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        c.device = dev;
+    }
+    const size_t n = static_cast<size_t>(nbytes);
+    char *dst = r2 ? r2 : region;
+    const int mode_add = r2 ? add : 0;
+    void *vs = device_view(region), *vd = device_view(dst);
+    if (vs && vd) {  // device-resident (or pinned/mapped): run in place
+        DROPIN_CHECK(cec_region_multiply(vs, multby, n, vd, mode_add, c.stream));
+        DROPIN_HIP(hipStreamSynchronize(c.stream));
+        return;
+    }
+    // pageable host buffers: stage through device memory chunk by chunk
+    const size_t want = std::min(n, kStageChunk);
+    if (c.cap < want) {
+        if (c.dsrc) DROPIN_HIP(hipFree(c.dsrc));
+        if (c.ddst) DROPIN_HIP(hipFree(c.ddst));
+        c.dsrc = c.ddst = nullptr;
+        DROPIN_HIP(hipMalloc(&c.dsrc, want));
+        DROPIN_HIP(hipMalloc(&c.ddst, want));
+        c.cap = want;
+    }
+    for (size_t o = 0; o < n; o += kStageChunk) {
+        const size_t len = std::min(kStageChunk, n - o);
+        DROPIN_HIP(hipMemcpyAsync(c.dsrc, region + o, len, hipMemcpyHostToDevice, c.stream));
+        if (mode_add)
+            DROPIN_HIP(hipMemcpyAsync(c.ddst, dst + o, len, hipMemcpyHostToDevice, c.stream));
+        DROPIN_CHECK(cec_region_multiply(c.dsrc, multby, len, c.ddst, mode_add, c.stream));
+        DROPIN_HIP(hipMemcpyAsync(dst + o, c.ddst, len, hipMemcpyDeviceToHost, c.stream));
+        DROPIN_HIP(hipStreamSynchronize(c.stream));
+    }
+}

@@ -1,0 +1,374 @@
+"""Python mirror of libcocytus_ec.so (include/cocytus_ec.h + the Jerasure drop-in).
+
+Thin ctypes bindings: the product is the C-ABI library; this module only marshals
+arguments and raises on error.  There is no Python or CPU implementation of any
+region arithmetic here -- if the shared library (or a gfx950 GPU) is missing, calls
+fail loudly.
+
+Device memory is passed as integer device pointers; anything with ``data_ptr()``
+(torch tensors) is accepted too.  When torch is used in the same process, import it
+BEFORE calling :func:`lib` so that both share one HIP runtime (checked).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, Sequence
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcocytus_ec.so")
+
+CEC_OK = 0
+CEC_EINVAL = -1
+CEC_ESINGULAR = -2
+CEC_EHIP = -3
+CEC_ENOMEM = -4
+CEC_EOVERLAP = -5
+CEC_ENODEV = -6
+CEC_ENGINE_PERM = 0
+CEC_ENGINE_LDS = 1
+CEC_MAX_K = 16
+CEC_MAX_M = 8
+UNIT_SIZE = 4096
+
+_STATUS = {
+    CEC_EINVAL: "CEC_EINVAL",
+    CEC_ESINGULAR: "CEC_ESINGULAR",
+    CEC_EHIP: "CEC_EHIP",
+    CEC_ENOMEM: "CEC_ENOMEM",
+    CEC_EOVERLAP: "CEC_EOVERLAP",
+    CEC_ENODEV: "CEC_ENODEV",
+}
+
+
+class CecError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{_STATUS.get(code, code)}: {msg}")
+        self.code = code
+
+
+class Extent(ctypes.Structure):
+    """cec_extent: one value of a batch (off: arena offset, src_off: staging offset)."""
+
+    _fields_ = [
+        ("off", ctypes.c_uint64),
+        ("src_off", ctypes.c_uint64),
+        ("len", ctypes.c_uint32),
+        ("pattern", ctypes.c_uint32),
+    ]
+
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_u32 = ctypes.c_uint32
+_ip = ctypes.POINTER(ctypes.c_int)
+_pp = ctypes.POINTER(ctypes.c_void_p)
+
+_SIGS = {
+    "cec_version": ([], ctypes.c_char_p),
+    "cec_last_error": ([], ctypes.c_char_p),
+    "cec_device_check": ([], _i),
+    "cec_set_engine": ([_i], _i),
+    "cec_get_engine": ([], _i),
+    "cec_plan_create": ([ctypes.POINTER(_vp), ctypes.POINTER(Extent), _i, _vp], _i),
+    "cec_plan_destroy": ([_vp], _i),
+    "cec_plan_num_extents": ([_vp], _i),
+    "cec_plan_num_tiles": ([_vp], ctypes.c_int64),
+    "cec_plan_total_bytes": ([_vp], ctypes.c_uint64),
+    "cec_region_multiply": ([_vp, _i, ctypes.c_size_t, _vp, _i, _vp], _i),
+    "cec_encode": ([_i, _i, _ip, _pp, _pp, _vp, _vp], _i),
+    "cec_encode_region": ([_i, _i, _ip, _pp, _pp, ctypes.c_size_t, _vp], _i),
+    "cec_diff_update": ([_i, _i, _ip, _pp, _vp, _pp, _i, _vp, _vp], _i),
+    "cec_set_diff": ([_i, _pp, _vp, _vp, _vp, _vp], _i),
+    "cec_apply_diffs": ([_i, _i, _ip, _i, _vp, _vp, _vp, _vp], _i),
+    "cec_residual": ([_i, _i, _ip, _i, _u32, _pp, _vp, _vp, _vp], _i),
+    "cec_solve": ([_i, _i, _ip, _u32, _pp, _pp, _vp, _vp], _i),
+    "cec_decode": ([_i, _i, _ip, ctypes.POINTER(_u32), _i, _pp, _pp, _vp, _vp], _i),
+    "cec_recovery_mask": ([_i, _i, _i, _ip], _u32),
+    "cec_event_create": ([ctypes.POINTER(_vp)], _i),
+    "cec_event_destroy": ([_vp], _i),
+    "cec_event_record": ([_vp, _vp], _i),
+    "cec_event_elapsed_ms": ([_vp, _vp, ctypes.POINTER(ctypes.c_float)], _i),
+    "cec_stream_synchronize": ([_vp], _i),
+    "galois_w08_region_multiply": ([_vp, _i, _i, _vp, _i], None),
+    "galois_single_multiply": ([_i, _i, _i], _i),
+    "galois_single_divide": ([_i, _i, _i], _i),
+    "galois_inverse": ([_i, _i], _i),
+    "reed_sol_big_vandermonde_distribution_matrix": ([_i, _i, _i], _ip),
+    "reed_sol_extended_vandermonde_matrix": ([_i, _i, _i], _ip),
+    "jerasure_invert_matrix": ([_ip, _ip, _i, _i], _i),
+    "jerasure_matrix_multiply": ([_ip, _ip, _i, _i, _i, _i, _i], _ip),
+}
+
+_lib = None
+
+
+def _hip_runtimes() -> set[str]:
+    """Distinct libamdhip64 files mapped into this process."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                if "libamdhip64" in line:
+                    paths.add(os.path.realpath(line.split()[-1]))
+    except OSError:
+        pass
+    return paths
+
+
+def lib() -> ctypes.CDLL:
+    """Load libcocytus_ec.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} is missing: build it with `python cocytus_amd/build.py` "
+            "(there is no CPU fallback)"
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (args, res) in _SIGS.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    libc = ctypes.CDLL(None)
+    libc.free.argtypes = [_vp]
+    L._free = libc.free
+    rts = _hip_runtimes()
+    if len(rts) > 1:
+        raise RuntimeError(
+            "two HIP runtimes are mapped (%s): import torch before loading cocytus_amd" % sorted(rts)
+        )
+    _lib = L
+    return L
+
+
+def _check(rc: int) -> None:
+    if rc != CEC_OK:
+        raise CecError(rc, lib().cec_last_error().decode(errors="replace"))
+
+
+def _ptr(x) -> int:
+    if x is None:
+        return 0
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return int(x.data_ptr())
+    raise TypeError(f"cannot take a device pointer of {type(x)!r}")
+
+
+def _stream(s) -> int:
+    if s is None:
+        return 0
+    if isinstance(s, int):
+        return s
+    if hasattr(s, "cuda_stream"):
+        return int(s.cuda_stream)
+    raise TypeError(f"not a stream: {type(s)!r}")
+
+
+def _ptr_array(xs: Iterable) -> ctypes.Array:
+    xs = list(xs)
+    return (ctypes.c_void_p * len(xs))(*[_ptr(x) or None for x in xs])
+
+
+def _int_array(xs: Sequence[int]) -> ctypes.Array:
+    return (ctypes.c_int * len(xs))(*[int(v) for v in xs])
+
+
+# ------------------------------------------------------------------ runtime
+def version() -> str:
+    return lib().cec_version().decode()
+
+
+def device_check() -> int:
+    return lib().cec_device_check()
+
+
+def set_engine(engine: int) -> None:
+    _check(lib().cec_set_engine(engine))
+
+
+def get_engine() -> int:
+    return lib().cec_get_engine()
+
+
+class Plan:
+    """A device-resident batch of extents (cec_plan)."""
+
+    def __init__(self, extents: Sequence[tuple] | ctypes.Array, stream=None):
+        if isinstance(extents, ctypes.Array):
+            arr = extents
+        else:
+            arr = (Extent * len(extents))(*[Extent(*e) for e in extents])
+        self._h = ctypes.c_void_p()
+        _check(lib().cec_plan_create(ctypes.byref(self._h), arr, len(arr), _vp(_stream(stream))))
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if not self._h:
+            raise ValueError("plan destroyed")
+        return self._h
+
+    @property
+    def num_extents(self) -> int:
+        return lib().cec_plan_num_extents(self.handle)
+
+    @property
+    def num_tiles(self) -> int:
+        return lib().cec_plan_num_tiles(self.handle)
+
+    @property
+    def total_bytes(self) -> int:
+        return lib().cec_plan_total_bytes(self.handle)
+
+    def destroy(self) -> None:
+        if self._h:
+            _check(lib().cec_plan_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.cec_plan_destroy(self._h)
+        except Exception:
+            pass
+
+
+def extents_array(rows: Iterable[tuple]) -> ctypes.Array:
+    rows = list(rows)
+    return (Extent * len(rows))(*[Extent(*r) for r in rows])
+
+
+# ------------------------------------------------------------------ ops
+def region_multiply(src, multby: int, nbytes: int, dst, add: int = 1, stream=None) -> None:
+    _check(lib().cec_region_multiply(_ptr(src), multby, nbytes, _ptr(dst) or None, add, _stream(stream)))
+
+
+def encode(k, m, matrix, data, parity, plan: Plan, stream=None) -> None:
+    _check(lib().cec_encode(k, m, _int_array(matrix), _ptr_array(data), _ptr_array(parity),
+                            plan.handle, _stream(stream)))
+
+
+def encode_region(k, m, matrix, data, parity, length: int, stream=None) -> None:
+    _check(lib().cec_encode_region(k, m, _int_array(matrix), _ptr_array(data), _ptr_array(parity),
+                                   length, _stream(stream)))
+
+
+def diff_update(k, m, matrix, data, staging, parity, install: bool, plan: Plan, stream=None) -> None:
+    _check(lib().cec_diff_update(k, m, _int_array(matrix), _ptr_array(data), _ptr(staging),
+                                 _ptr_array(parity), int(bool(install)), plan.handle, _stream(stream)))
+
+
+def set_diff(k, data, staging, diff, plan: Plan, stream=None) -> None:
+    _check(lib().cec_set_diff(k, _ptr_array(data), _ptr(staging), _ptr(diff), plan.handle,
+                              _stream(stream)))
+
+
+def apply_diffs(k, m, matrix, lid_self, diffs, parity, plan: Plan, stream=None) -> None:
+    _check(lib().cec_apply_diffs(k, m, _int_array(matrix), lid_self, _ptr(diffs), _ptr(parity),
+                                 plan.handle, _stream(stream)))
+
+
+def residual(k, m, matrix, lid_self, mask, arenas, out, plan: Plan, stream=None) -> None:
+    _check(lib().cec_residual(k, m, _int_array(matrix), lid_self, mask, _ptr_array(arenas), _ptr(out),
+                              plan.handle, _stream(stream)))
+
+
+def solve(k, m, matrix, mask, residuals, out, plan: Plan, stream=None) -> None:
+    _check(lib().cec_solve(k, m, _int_array(matrix), mask, _ptr_array(residuals), _ptr_array(out),
+                           plan.handle, _stream(stream)))
+
+
+def decode(k, m, matrix, masks: Sequence[int], arenas, out, plan: Plan, stream=None) -> None:
+    marr = (ctypes.c_uint32 * len(masks))(*[int(x) for x in masks])
+    _check(lib().cec_decode(k, m, _int_array(matrix), marr, len(masks), _ptr_array(arenas),
+                            _ptr_array(out), plan.handle, _stream(stream)))
+
+
+def recovery_mask(k: int, m: int, leader_lid: int, connected: Sequence[int]) -> int:
+    return lib().cec_recovery_mask(k, m, leader_lid, _int_array(connected))
+
+
+class Event:
+    def __init__(self):
+        self._e = ctypes.c_void_p()
+        _check(lib().cec_event_create(ctypes.byref(self._e)))
+
+    def record(self, stream=None) -> None:
+        _check(lib().cec_event_record(self._e, _stream(stream)))
+
+    def elapsed_ms(self, end: "Event") -> float:
+        ms = ctypes.c_float()
+        _check(lib().cec_event_elapsed_ms(self._e, end._e, ctypes.byref(ms)))
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            if self._e and _lib is not None:
+                _lib.cec_event_destroy(self._e)
+        except Exception:
+            pass
+
+
+def stream_synchronize(stream=None) -> None:
+    _check(lib().cec_stream_synchronize(_stream(stream)))
+
+
+# ------------------------------------------------------------------ Jerasure drop-in
+def galois_w08_region_multiply(region, multby: int, nbytes: int, r2, add: int) -> None:
+    """The drop-in symbol itself (host or device buffers; synchronous; aborts on error).
+
+    region / r2: device pointers (int / tensor) or writable host buffers (bytearray,
+    numpy arrays) -- host buffers are passed by address.
+    """
+    lib().galois_w08_region_multiply(_host_or_dev(region), multby, nbytes, _host_or_dev(r2), add)
+
+
+def _host_or_dev(x):
+    if x is None:
+        return None
+    if isinstance(x, (bytearray, memoryview)):
+        return ctypes.addressof(ctypes.c_char.from_buffer(x))
+    if hasattr(x, "ctypes") and hasattr(x, "dtype"):  # numpy
+        return x.ctypes.data
+    return _ptr(x)
+
+
+def galois_single_multiply(a: int, b: int, w: int = 8) -> int:
+    return lib().galois_single_multiply(a, b, w)
+
+
+def galois_single_divide(a: int, b: int, w: int = 8) -> int:
+    return lib().galois_single_divide(a, b, w)
+
+
+def reed_sol_big_vandermonde_distribution_matrix(rows: int, cols: int, w: int = 8) -> list[int] | None:
+    p = lib().reed_sol_big_vandermonde_distribution_matrix(rows, cols, w)
+    if not p:
+        return None
+    out = [p[i] for i in range(rows * cols)]
+    lib()._free(ctypes.cast(p, ctypes.c_void_p))
+    return out
+
+
+def jerasure_invert_matrix(mat: Sequence[int], rows: int, w: int = 8) -> tuple[int, list[int]]:
+    a = _int_array(mat)
+    inv = (ctypes.c_int * (rows * rows))()
+    rc = lib().jerasure_invert_matrix(a, inv, rows, w)
+    return rc, list(inv)
+
+
+def coding_matrix(k: int, m: int) -> list[int]:
+    """MATRIX of memcached.c:6845: reed_sol_big_vandermonde_distribution_matrix(k+m, k, 8)."""
+    mat = reed_sol_big_vandermonde_distribution_matrix(k + m, k, 8)
+    if mat is None:
+        raise CecError(CEC_EINVAL, f"no coding matrix for k={k} m={m}")
+    return mat

@@ -1,0 +1,162 @@
+/*
+ * cocytus_ec.h -- batched, device-resident erasure-coding API of libcocytus_ec.so
+ * (MI355X / gfx950, hand-written HIP kernels; no MFMA, no Jerasure).
+ *
+ * This is the additive entry-point set SURVEY.md §8(b) asks for next to the three
+ * drop-in Jerasure symbols (galois.h / jerasure.h / reed_sol.h).  Every call is
+ * asynchronous on the given HIP stream (NULL = the default stream), takes device
+ * pointers only, and returns a cec_status.  Nothing here falls back to the CPU:
+ * a missing GPU is CEC_ENODEV.
+ *
+ * Layout contract (Cocytus): every data shard j and every parity p owns an arena
+ * (ecmem, /root/reference/ecmem.h:29-58).  A value is the byte range
+ * [off, off+len) of an arena; parity bytes sit at the SAME offset as the data
+ * they encode (/root/reference/memcached.c:7704-7717), offsets are 16-B aligned
+ * (/root/reference/ecalloc.c:176) and recovery works on 4 KiB units
+ * (/root/reference/const.h:26).  Unaligned offsets and lengths are accepted
+ * (slower byte path for the affected tiles), bit-exact either way.
+ *
+ * Coding matrix: int[(k+m)*k], row-major, MATRIX(x,y) = matrix[x*k+y]
+ * (/root/reference/memcached.h:52), as returned by
+ * reed_sol_big_vandermonde_distribution_matrix(k+m, k, 8)
+ * (/root/reference/memcached.c:6845).  Limits: 1 <= k <= CEC_MAX_K,
+ * 1 <= m <= CEC_MAX_M, k+m <= 32 (Cocytus masks are uint32_t).
+ */
+#ifndef COCYTUS_EC_H
+#define COCYTUS_EC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CEC_MAX_K 16
+#define CEC_MAX_M 8
+#define CEC_UNIT_SIZE 4096 /* UNITSIZE, /root/reference/const.h:26; also the kernel tile */
+
+typedef enum cec_status {
+    CEC_OK = 0,
+    CEC_EINVAL = -1,      /* bad argument (k/m/lid/mask/pointer/pattern index) */
+    CEC_ESINGULAR = -2,   /* decode submatrix not invertible (memcached.c:7908 asserts) */
+    CEC_EHIP = -3,        /* a HIP runtime call failed; see cec_last_error() */
+    CEC_ENOMEM = -4,      /* device or pinned-host allocation failed */
+    CEC_EOVERLAP = -5,    /* read-modify-write op on a plan whose extents overlap */
+    CEC_ENODEV = -6       /* no usable gfx950 device: there is no CPU fallback */
+} cec_status;
+
+/* One value of a batch.  `off` addresses the arenas (item->addr, memcached.h:441);
+ * `src_off` addresses the staging buffer that carries values from / to the network
+ * (c->vbuf, e->vbuf: memcached.c:3646-3655, 7727-7735); `pattern` is per-op:
+ *   cec_diff_update / cec_apply_diffs : source data shard lid j (0..k-1)
+ *   cec_decode                         : index into the op's mask array
+ *   other ops                          : ignored (0). */
+typedef struct cec_extent {
+    uint64_t off;
+    uint64_t src_off;
+    uint32_t len;
+    uint32_t pattern;
+} cec_extent;
+
+/* A device-resident batch: the extents plus the 4 KiB tile work-list the kernels
+ * walk (load balance across mixed 256 B .. 1 MiB values).  Build once per batch. */
+typedef struct cec_plan cec_plan;
+
+/* GF(2^8) engine used by the kernels.  Both are bit-exact; PERM (default) looks up
+ * three 8-entry byte tables per coefficient with v_perm_b32 (pure VALU); LDS is the
+ * 256-entry log / antilog tables staged in LDS (two ds_read_u8 per byte). */
+typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1 } cec_engine;
+
+/* ---- runtime ---- */
+const char *cec_version(void);
+const char *cec_last_error(void);               /* thread-local message of the last failure */
+int cec_device_check(void);                     /* CEC_OK if the current device is gfx950 */
+int cec_set_engine(cec_engine e);               /* process-wide; default CEC_ENGINE_PERM */
+cec_engine cec_get_engine(void);
+
+/* ---- plans ---- */
+/* extents: HOST array of n cec_extent (n >= 0).  The tile list is built on the host
+ * and copied to the device on `stream`; the plan is usable by later calls on any
+ * stream ordered after it.  Overlapping [off, off+len) ranges are recorded: RMW ops
+ * (cec_diff_update, cec_apply_diffs) refuse such a plan with CEC_EOVERLAP. */
+int cec_plan_create(cec_plan **out, const cec_extent *extents, int n, void *stream);
+int cec_plan_destroy(cec_plan *plan);           /* synchronises with pending work */
+int cec_plan_num_extents(const cec_plan *plan);
+int64_t cec_plan_num_tiles(const cec_plan *plan);
+uint64_t cec_plan_total_bytes(const cec_plan *plan); /* sum of extent lengths */
+
+/* ---- ops (all async on `stream`) ---- */
+
+/* Device form of galois_w08_region_multiply:
+ * add != 0: dst[i] ^= c*src[i]; add == 0: dst[i] = c*src[i]; dst == NULL: in place. */
+int cec_region_multiply(const void *src, int multby, size_t nbytes, void *dst, int add,
+                        void *stream);
+
+/* Full-stripe encode over arena extents (a5): parity[p][off..] = sum_j
+ * MATRIX(k+p, j) * data[j][off..].  data: k device arena bases, parity: m. */
+int cec_encode(int k, int m, const int *matrix, const uint8_t *const *data,
+               uint8_t *const *parity, const cec_plan *plan, void *stream);
+
+/* Encode one contiguous range [0, len) of every arena (no plan needed). */
+int cec_encode_region(int k, int m, const int *matrix, const uint8_t *const *data,
+                      uint8_t *const *parity, size_t len, void *stream);
+
+/* Fused per-SET diff-update (a4 = a2 + M x a3): for each extent with source shard
+ * j = pattern: d = staging[src_off..] ^ data[j][off..]; parity[p][off..] ^=
+ * MATRIX(k+p, j) * d for every p with parity[p] != NULL (a lost parity is
+ * skipped, memcached.c:2692-2694); if install, data[j][off..] = new value
+ * (memcached.c:5666).  Extents must not overlap (CEC_EOVERLAP). */
+int cec_diff_update(int k, int m, const int *matrix, uint8_t *const *data,
+                    const uint8_t *staging, uint8_t *const *parity, int install,
+                    const cec_plan *plan, void *stream);
+
+/* Data-side diff only (memcached.c:2673-2681): diff[src_off..] = staging[src_off..]
+ * ^ data[pattern][off..].  diff and staging share src_off addressing. */
+int cec_set_diff(int k, const uint8_t *const *data, const uint8_t *staging, uint8_t *diff,
+                 const cec_plan *plan, void *stream);
+
+/* Parity-side deferred apply of shipped diffs (memcached.c:7762-7767, the drain
+ * loops at :4231, :4322, :4350, :8068): parity[off..] ^= MATRIX(lid_self, j) *
+ * diffs[src_off..] with j = pattern.  Extents must not overlap (CEC_EOVERLAP). */
+int cec_apply_diffs(int k, int m, const int *matrix, int lid_self, const uint8_t *diffs,
+                    uint8_t *parity, const cec_plan *plan, void *stream);
+
+/* Recovery residual on parity lid_self (recovery.c:61-96): residual[off..] =
+ * arenas[lid_self][off..] ^ sum_{data lid s in mask, s != lid_self}
+ * MATRIX(lid_self, s) * arenas[s][off..].  arenas: k+m bases indexed by lid (only
+ * the ones the mask names are read). */
+int cec_residual(int k, int m, const int *matrix, int lid_self, uint32_t mask,
+                 const uint8_t *const *arenas, uint8_t *residual, const cec_plan *plan,
+                 void *stream);
+
+/* Leader solve (memcached.c:7842-7922): with n lost data lids (not in mask) and the
+ * n parities in mask, out[lost_i][off..] = sum_r inv[i][r] * residuals[par_r][off..].
+ * residuals: k+m bases indexed by parity lid; out: k bases indexed by data lid. */
+int cec_solve(int k, int m, const int *matrix, uint32_t mask,
+              const uint8_t *const *residuals, uint8_t *const *out, const cec_plan *plan,
+              void *stream);
+
+/* Fused online recovery (residual + solve in one pass, bit-exact because GF(2^8)
+ * arithmetic is exact): for each extent, mask = masks[pattern]; every data lid not
+ * in the mask is rebuilt into out[lid][off..] from the k participants' arenas.
+ * masks follow start_recovery (memcached.c:8136-8151): exactly k lids. */
+int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, int n_masks,
+               const uint8_t *const *arenas, uint8_t *const *out, const cec_plan *plan,
+               void *stream);
+
+/* Mask helper identical to start_recovery (memcached.c:8136-8151).  connected:
+ * k+m ints.  Returns 0 if fewer than k lids are available. */
+uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected);
+
+/* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
+int cec_event_create(void **ev);
+int cec_event_destroy(void *ev);
+int cec_event_record(void *ev, void *stream);
+int cec_event_elapsed_ms(void *start, void *stop, float *ms); /* synchronises on stop */
+int cec_stream_synchronize(void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* COCYTUS_EC_H */

@@ -1,0 +1,161 @@
+/*
+ * oracle/gf8_cpu_baseline.c -- the timed CPU baseline (bench.py cpu_baseline leg).
+ *
+ * TEST / MEASUREMENT INFRASTRUCTURE ONLY; never linked into the product.
+ *
+ * The reference CPU path is Jerasure + GF-Complete, absent from this image
+ * (SURVEY.md §8c), so this is the "restated CPU baseline": GF-Complete's default
+ * w=8 region multiply (SPLIT 8,4: two 16-entry product tables per coefficient,
+ * one per nibble, looked up with pshufb) restated with 32-byte AVX2 vpshufb, and
+ * chained exactly like the reference's call sites:
+ *   encode  = K SETs into zero parity, one region multiply per (parity, shard)
+ *             (memcached.c:2681 + 7764 with old = 0);
+ *   decode  = residual build per survivor (recovery.c:79-93) + leader solve
+ *             (memcached.c:7913-7922) into a zeroed buffer.
+ */
+#include "gf8_ref.h"
+
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#if defined(__x86_64__)
+#include <immintrin.h>
+#define HAVE_X86 1
+#endif
+
+int ref_simd_available(void)
+{
+#if HAVE_X86
+    __builtin_cpu_init();
+    return __builtin_cpu_supports("avx2") ? 1 : 0;
+#else
+    return 0;
+#endif
+}
+
+#if HAVE_X86
+__attribute__((target("avx2")))
+static void region_mul_xor_avx2(const uint8_t *src, int c, long n, uint8_t *dst)
+{
+    uint8_t lo[16], hi[16];
+    for (int i = 0; i < 16; ++i) {
+        lo[i] = (uint8_t)ref_gf_mul(c, i);
+        hi[i] = (uint8_t)ref_gf_mul(c, i << 4);
+    }
+    const __m256i tlo = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)lo));
+    const __m256i thi = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i *)hi));
+    const __m256i mask = _mm256_set1_epi8(0x0F);
+    long i = 0;
+    if (c == 1) {
+        for (; i + 32 <= n; i += 32) {
+            __m256i s = _mm256_loadu_si256((const __m256i *)(src + i));
+            __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+            _mm256_storeu_si256((__m256i *)(dst + i), _mm256_xor_si256(s, d));
+        }
+    } else {
+        for (; i + 32 <= n; i += 32) {
+            __m256i s = _mm256_loadu_si256((const __m256i *)(src + i));
+            __m256i d = _mm256_loadu_si256((const __m256i *)(dst + i));
+            __m256i l = _mm256_shuffle_epi8(tlo, _mm256_and_si256(s, mask));
+            __m256i h = _mm256_shuffle_epi8(thi, _mm256_and_si256(_mm256_srli_epi64(s, 4), mask));
+            d = _mm256_xor_si256(d, _mm256_xor_si256(l, h));
+            _mm256_storeu_si256((__m256i *)(dst + i), d);
+        }
+    }
+    for (; i < n; ++i) dst[i] ^= (uint8_t)(lo[src[i] & 15] ^ hi[src[i] >> 4]);
+}
+#endif
+
+void ref_region_multiply_simd(const uint8_t *region, int multby, long nbytes, uint8_t *r2)
+{
+    if (multby == 0 || nbytes <= 0) return;
+#if HAVE_X86
+    if (ref_simd_available()) { region_mul_xor_avx2(region, multby, nbytes, r2); return; }
+#endif
+    ref_region_multiply((uint8_t *)region, multby, nbytes, r2, 1);
+}
+
+typedef struct {
+    const int *matrix;
+    int k, m, do_decode, reps;
+    long n, s0, s1;
+    uint8_t **data, **parity, *out, *res;
+    pthread_barrier_t *bar;
+} bench_arg;
+
+static void *bench_worker(void *p)
+{
+    bench_arg *a = (bench_arg *)p;
+    const int k = a->k, m = a->m;
+    const long n = a->n;
+    pthread_barrier_wait(a->bar);
+    for (int r = 0; r < a->reps; ++r) {
+        for (long s = a->s0; s < a->s1; ++s) {
+            const long off = s * n;
+            for (int q = 0; q < m; ++q) memset(a->parity[q] + off, 0, (size_t)n);
+            for (int j = 0; j < k; ++j)
+                for (int q = 0; q < m; ++q)
+                    ref_region_multiply_simd(a->data[j] + off, a->matrix[(k + q) * k + j], n,
+                                             a->parity[q] + off);
+            if (!a->do_decode) continue;
+            /* one lost data shard per stripe, leader parity rotates */
+            const int lost = (int)(s % k), leader = k + (int)((s / k) % m);
+            memcpy(a->res, a->parity[leader - k] + off, (size_t)n);
+            for (int j = 0; j < k; ++j)
+                if (j != lost)
+                    ref_region_multiply_simd(a->data[j] + off, a->matrix[leader * k + j], n, a->res);
+            const int inv = ref_gf_div(1, a->matrix[leader * k + lost]);
+            memset(a->out, 0, (size_t)n);
+            ref_region_multiply_simd(a->res, inv, n, a->out);
+        }
+    }
+    return NULL;
+}
+
+double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
+                               int reps, int do_decode)
+{
+    if (threads < 1) threads = 1;
+    int *matrix = ref_big_vandermonde(k + m, k);
+    uint8_t *data[32], *parity[32];
+    const size_t bytes = (size_t)n * (size_t)nstripes;
+    for (int j = 0; j < k; ++j) {
+        data[j] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
+        uint64_t x = 0xC0C70001ull + (uint64_t)j;
+        for (size_t i = 0; i < bytes; i += 8) {   /* splitmix64 fill */
+            uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+            z ^= z >> 31;
+            memcpy(data[j] + i, &z, (bytes - i) < 8 ? (bytes - i) : 8);
+        }
+    }
+    for (int q = 0; q < m; ++q) parity[q] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
+    pthread_barrier_t bar;
+    pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+    pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
+    bench_arg *args = (bench_arg *)calloc((size_t)threads, sizeof(bench_arg));
+    for (int t = 0; t < threads; ++t) {
+        bench_arg *a = &args[t];
+        a->matrix = matrix; a->k = k; a->m = m; a->n = n; a->reps = reps; a->do_decode = do_decode;
+        a->s0 = nstripes * t / threads;
+        a->s1 = nstripes * (t + 1) / threads;
+        a->data = data; a->parity = parity; a->bar = &bar;
+        a->out = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
+        a->res = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
+        pthread_create(&tid[t], NULL, bench_worker, a);
+    }
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    pthread_barrier_wait(&bar);
+    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int t = 0; t < threads; ++t) { free(args[t].out); free(args[t].res); }
+    for (int j = 0; j < k; ++j) free(data[j]);
+    for (int q = 0; q < m; ++q) free(parity[q]);
+    free(args); free(tid); free(matrix);
+    pthread_barrier_destroy(&bar);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

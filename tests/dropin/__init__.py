@@ -1,0 +1,66 @@
+"""Drop-in check: a C program against include/{galois,jerasure,reed_sol}.h linked as
+-lJerasure (libJerasure.so -> libcocytus_ec.so) vs the oracle on the same inputs."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+LIBDIR = os.path.join(ROOT, "cocytus_amd")
+
+
+def build_dropin(out_dir: str) -> str:
+    exe = os.path.join(out_dir, "dropin_main")
+    subprocess.run(
+        ["gcc", "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
+         os.path.join(HERE, "dropin_main.c"), "-L", LIBDIR, "-lJerasure",
+         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+        check=True,
+    )
+    return exe
+
+
+def run_dropin_case(oracle, tmp_path, K=3, M=2, seed=0xC0C70001) -> None:
+    rng = np.random.default_rng(seed)
+    arena = 64 * 4096
+    nsets = 300
+    sets, vals = [], []
+    for _ in range(nsets):  # SETs may overlap: the chain is sequential, like the server
+        n = int(rng.integers(1, 6000)) + 2          # vlen + "\r\n"
+        addr = int(rng.integers(0, (arena - n) // 16)) * 16  # ecalloc.c:176
+        sets.append((int(rng.integers(0, K)), addr, n))
+        vals.append(rng.integers(0, 256, n, dtype=np.uint8))
+    mask = oracle.recovery_mask(K, M, K + 1, [1, 0, 1, 0, 1][: K + M])  # D1, P0 lost; leader P1
+    ub, ue = 3, 40
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        f.write(np.array([K, M, arena, nsets, ub, ue, mask], np.int32).tobytes())
+        f.write(np.array(sets, np.int32).tobytes())
+        for v in vals:
+            f.write(v.tobytes())
+    exe = build_dropin(str(tmp_path))
+    outp = tmp_path / "out.bin"
+    r = subprocess.run([exe, str(inp), str(outp)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr + r.stdout
+    got = np.fromfile(outp, np.uint8)
+
+    mat = oracle.big_vandermonde(K + M, K)
+    data = [np.zeros(arena, np.uint8) for _ in range(K)]
+    parity = [np.zeros(arena, np.uint8) for _ in range(M)]
+    for (j, addr, n), v in zip(sets, vals):
+        old = data[j][addr:addr + n].copy()
+        pv = [p[addr:addr + n].copy() for p in parity]
+        oracle.diff_update(mat, K, M, j, old, v, pv, True)
+        data[j][addr:addr + n] = old
+        for p in range(M):
+            parity[p][addr:addr + n] = pv[p]
+    lo, hi = ub * 4096, (ue + 1) * 4096
+    arenas = [a[lo:hi].copy() if (mask >> i) & 1 else None for i, a in enumerate(data + parity)]
+    rec = oracle.decode(mat, K, M, mask, arenas)
+    exp = np.concatenate(data + parity + rec)
+    assert got.size == exp.size
+    assert np.array_equal(got, exp)
+    assert np.array_equal(rec[0], data[1][lo:hi])  # the rebuilt shard is D1

@@ -1,0 +1,129 @@
+"""CPU checks of the C-ABI library: it loads without a GPU, exports every symbol the
+headers in include/ declare, its host-side matrix code (reed_sol / jerasure_invert)
+agrees with the oracle, and every compute entry point fails loudly (no CPU fallback)
+when there is no GPU."""
+from __future__ import annotations
+
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = ["cocytus_ec.h", "galois.h", "jerasure.h", "reed_sol.h"]
+
+
+def declared_functions() -> set[str]:
+    names = set()
+    for h in HEADERS:
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"\b([a-z_][a-z0-9_]*)\s*\(", src):
+            name = m.group(1)
+            if name.startswith(("cec_", "galois_", "reed_sol_", "jerasure_")):
+                names.add(name)
+    return names
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from cocytus_amd import build, ec
+
+    build.build(verbose=False)
+    return ec
+
+
+def exported_symbols(path: str) -> set[str]:
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True, check=True)
+    return {line.split()[-1] for line in out.stdout.splitlines() if " T " in line}
+
+
+def test_exports_every_declared_symbol(lib):
+    decl = declared_functions()
+    assert {"galois_w08_region_multiply", "reed_sol_big_vandermonde_distribution_matrix",
+            "jerasure_invert_matrix", "cec_encode", "cec_decode", "cec_diff_update"} <= decl
+    syms = exported_symbols(lib.LIB_PATH)
+    missing = decl - syms
+    assert not missing, missing
+    lib.lib()  # every binding resolves
+    # -lJerasure drop-in name
+    assert os.path.realpath(os.path.join(ROOT, "cocytus_amd", "libJerasure.so")) == os.path.realpath(lib.LIB_PATH)
+
+
+def test_no_internal_symbols_leak(lib):
+    syms = exported_symbols(lib.LIB_PATH)
+    ours = {s for s in syms if not s.startswith(("cec_", "galois_", "reed_sol_", "jerasure_", "_"))}
+    assert not {s for s in ours if "combine" in s or "cec" in s.lower()}
+
+
+@pytest.mark.parametrize("k,m", [(1, 1), (2, 1), (3, 2), (4, 2), (6, 3), (10, 4), (12, 8), (16, 16)])
+def test_coding_matrix_matches_oracle(lib, oracle, k, m):
+    assert lib.reed_sol_big_vandermonde_distribution_matrix(k + m, k, 8) == oracle.big_vandermonde(k + m, k)
+
+
+def test_coding_matrix_known_answers(lib):
+    # SURVEY.md §8c restated known answers (parity rows only)
+    assert lib.coding_matrix(3, 2)[9:] == [1, 1, 1, 1, 245, 244]
+    assert lib.coding_matrix(4, 2)[16:] == [1, 1, 1, 1, 1, 70, 143, 200]
+    assert lib.reed_sol_big_vandermonde_distribution_matrix(3, 3, 8) is None
+    assert lib.reed_sol_big_vandermonde_distribution_matrix(5, 3, 16) is None
+
+
+def test_invert_matches_oracle(lib, oracle):
+    import numpy as np
+
+    rng = np.random.default_rng(9)
+    for n in [1, 2, 3, 4, 6, 8]:
+        for _ in range(30):
+            mat = [int(x) for x in rng.integers(0, 256, n * n)]
+            if rng.random() < 0.2:
+                mat[: n] = [0] * n  # singular
+            r1, inv1 = lib.jerasure_invert_matrix(mat, n, 8)
+            r2, inv2 = oracle.invert(mat, n)
+            assert r1 == r2
+            if r1 == 0:
+                assert inv1 == inv2
+
+
+def test_single_ops(lib, oracle):
+    for a in range(0, 256, 7):
+        for b in range(0, 256, 5):
+            assert lib.galois_single_multiply(a, b, 8) == oracle.gf_mul(a, b)
+            assert lib.galois_single_divide(a, b, 8) == oracle.gf_div(a, b)
+
+
+def test_compute_fails_loudly_without_gpu(lib):
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present: covered by the gpu tests")
+    assert lib.device_check() == lib.CEC_ENODEV
+    with pytest.raises(lib.CecError) as ei:
+        lib.Plan([(0, 0, 4096, 0)])
+    assert ei.value.code == lib.CEC_ENODEV
+    with pytest.raises(lib.CecError):
+        lib.region_multiply(0x1000, 2, 16, 0x2000, 1)
+    with pytest.raises(lib.CecError):
+        lib.encode_region(3, 2, lib.coding_matrix(3, 2), [0x1000] * 3, [0x2000] * 2, 4096)
+    # the void drop-in aborts with a message instead of computing on the CPU
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np\nfrom cocytus_amd import ec\n"
+            "a = np.ones(64, np.uint8); b = np.zeros(64, np.uint8)\n"
+            "ec.galois_w08_region_multiply(a, 2, 64, b, 1)\nprint('computed')\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "computed" not in r.stdout
+    assert "libcocytus_ec: fatal" in r.stderr
+
+
+def test_bad_arguments_rejected(lib):
+    mat = lib.coding_matrix(3, 2)
+    with pytest.raises(lib.CecError) as ei:
+        lib.encode_region(0, 2, mat, [], [0, 0], 16)
+    assert ei.value.code == lib.CEC_EINVAL
+    with pytest.raises(lib.CecError) as ei:
+        lib.encode_region(17, 2, [1] * 19 * 17, [0] * 17, [0, 0], 16)
+    assert ei.value.code == lib.CEC_EINVAL
+    assert lib.recovery_mask(3, 2, 3, [1, 1, 1, 1, 1]) == 0b01011
+    assert lib.recovery_mask(3, 2, 3, [0, 0, 1, 1, 0]) == 0

@@ -1,0 +1,437 @@
+"""GPU parity: every op of libcocytus_ec.so (called through its C-ABI) against the
+CPU restatement in oracle/ on the same seeded inputs.  Bit-exact (byte arithmetic).
+
+Parity is "unpinned" (see oracle/gf8_ref.h): the reference's Jerasure/GF-Complete is
+not available, so the oracle restates it; tests/test_oracle.py pins the oracle to the
+independent known answers that exist.
+"""
+from __future__ import annotations
+
+import itertools
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CODES = [(3, 2), (4, 2), (6, 3), (10, 4), (16, 4), (2, 5)]
+SENT = 0xA5
+
+
+@pytest.fixture(params=["perm", "lds"])
+def engine(request, gpu):
+    torch, ec = gpu
+    ec.set_engine(ec.CEC_ENGINE_PERM if request.param == "perm" else ec.CEC_ENGINE_LDS)
+    yield request.param
+    ec.set_engine(ec.CEC_ENGINE_PERM)
+
+
+def to_dev(torch, a: np.ndarray):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def to_host(t) -> np.ndarray:
+    return t.cpu().numpy()
+
+
+def make_extents(rng, lens, align=16, gap=48, unaligned_every=0):
+    """Non-overlapping extents laid out like ecalloc (16-B aligned starts)."""
+    ext, off, soff = [], 64, 32
+    for i, n in enumerate(lens):
+        o = off
+        if unaligned_every and i % unaligned_every == unaligned_every - 1:
+            o += 1 + int(rng.integers(0, 15))  # deliberately misaligned arena offset
+        ext.append([o, soff, n, 0])
+        off = ((o + n + gap + align - 1) // align) * align
+        soff = ((soff + n + 16 + 15) // 16) * 16
+    return ext, off, soff
+
+
+MIXED = [0, 1, 15, 16, 17, 255, 256, 4095, 4096, 4097, 4098, 8195, 65536, 100003, 1 << 20]
+
+
+# ------------------------------------------------------------------ region multiply (a1)
+@pytest.mark.parametrize("c", [0, 1, 2, 0x80, 244, 245, 255, 0x53])
+@pytest.mark.parametrize("add", [0, 1])
+def test_region_multiply_device(gpu, oracle, engine, c, add):
+    torch, ec = gpu
+    rng = np.random.default_rng(c * 2 + add)
+    for n in [1, 15, 16, 17, 4095, 4096, 4098, (1 << 20) + 3]:
+        for so, do in [(0, 0), (16, 32), (3, 3), (1, 7)]:
+            src = rng.integers(0, 256, n + 64, dtype=np.uint8)
+            dst = rng.integers(0, 256, n + 64, dtype=np.uint8)
+            exp = dst.copy()
+            view = exp[do:do + n].copy()
+            oracle.region_multiply(src[so:so + n].copy(), c, view, add)
+            exp[do:do + n] = view
+            ds, dd = to_dev(torch, src), to_dev(torch, dst)
+            ec.region_multiply(ds.data_ptr() + so, c, n, dd.data_ptr() + do, add)
+            torch.cuda.synchronize()
+            got = to_host(dd)
+            assert np.array_equal(got, exp), (c, add, n, so, do)
+
+
+def test_region_multiply_in_place(gpu, oracle):
+    torch, ec = gpu
+    a = oracle.splitmix_bytes(7, 9000)
+    exp = a.copy()
+    oracle.region_multiply(exp, 0x1D, None, 0)
+    d = to_dev(torch, a)
+    ec.region_multiply(d, 0x1D, 9000, None, 0)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(d), exp)
+
+
+# ------------------------------------------------------------------ encode (a5)
+@pytest.mark.parametrize("k,m", CODES)
+def test_encode_plan(gpu, oracle, engine, k, m):
+    torch, ec = gpu
+    mat = ec.coding_matrix(k, m)
+    assert mat == oracle.big_vandermonde(k + m, k)
+    rng = np.random.default_rng(1000 * k + m)
+    ext, arena_len, _ = make_extents(rng, MIXED, unaligned_every=5)
+    data = [rng.integers(0, 256, arena_len, dtype=np.uint8) for _ in range(k)]
+    par0 = np.full(arena_len, SENT, np.uint8)
+    ddev = [to_dev(torch, d) for d in data]
+    pdev = [to_dev(torch, par0) for _ in range(m)]
+    with ec.Plan([tuple(e) for e in ext]) as plan:
+        assert plan.num_extents == len(ext)
+        assert plan.total_bytes == sum(MIXED)
+        ec.encode(k, m, mat, ddev, pdev, plan)
+        torch.cuda.synchronize()
+    exp = [par0.copy() for _ in range(m)]
+    for off, _, n, _ in ext:
+        if n == 0:
+            continue
+        ps = oracle.encode(mat, k, m, [d[off:off + n].copy() for d in data])
+        for p in range(m):
+            exp[p][off:off + n] = ps[p]
+    for p in range(m):
+        assert np.array_equal(to_host(pdev[p]), exp[p]), f"parity {p}"
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (8, 4)])
+def test_encode_region(gpu, oracle, engine, k, m):
+    torch, ec = gpu
+    mat = ec.coding_matrix(k, m)
+    n = 3 * 4096 + 1234
+    data = [oracle.splitmix_bytes(0xC0C70001 + j, n) for j in range(k)]
+    pdev = [to_dev(torch, np.zeros(n, np.uint8)) for _ in range(m)]
+    ec.encode_region(k, m, mat, [to_dev(torch, d) for d in data], pdev, n)
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, data)
+    for p in range(m):
+        assert np.array_equal(to_host(pdev[p]), exp[p])
+
+
+def test_encode_lost_parity_not_written(gpu, oracle):
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    n = 8192
+    data = [oracle.splitmix_bytes(j + 1, n) for j in range(k)]
+    p0 = to_dev(torch, np.zeros(n, np.uint8))
+    ec.encode_region(k, m, mat, [to_dev(torch, d) for d in data], [p0, None], n)
+    torch.cuda.synchronize()
+    assert np.array_equal(to_host(p0), oracle.encode(mat, k, m, data)[0])
+
+
+# ------------------------------------------------------------------ diff-update (a2+a3)
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3), (2, 5)])
+@pytest.mark.parametrize("install", [False, True])
+def test_diff_update(gpu, oracle, engine, k, m, install):
+    torch, ec = gpu
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(77 + k * 10 + m + install)
+    lens = [int(x) for x in rng.integers(1, 20000, 40)] + [4098, 4096, 16, 17]
+    ext, arena_len, stage_len = make_extents(rng, lens, unaligned_every=7)
+    for e in ext:
+        e[3] = int(rng.integers(0, k))  # source data shard lid j
+    data = [rng.integers(0, 256, arena_len, dtype=np.uint8) for _ in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    staging = rng.integers(0, 256, stage_len, dtype=np.uint8)
+    ddev = [to_dev(torch, d) for d in data]
+    pdev = [to_dev(torch, p) for p in parity]
+    with ec.Plan([tuple(e) for e in ext]) as plan:
+        ec.diff_update(k, m, mat, ddev, to_dev(torch, staging), pdev, install, plan)
+        torch.cuda.synchronize()
+    for off, soff, n, j in ext:  # the reference chain, SET by SET
+        old = data[j][off:off + n].copy()
+        pv = [p[off:off + n].copy() for p in parity]
+        oracle.diff_update(mat, k, m, j, old, staging[soff:soff + n].copy(), pv, install)
+        data[j][off:off + n] = old
+        for p in range(m):
+            parity[p][off:off + n] = pv[p]
+    for j in range(k):
+        assert np.array_equal(to_host(ddev[j]), data[j]), f"data {j}"
+    for p in range(m):
+        assert np.array_equal(to_host(pdev[p]), parity[p]), f"parity {p}"
+    if install:  # parity is again the encode of the installed data
+        enc = oracle.encode(mat, k, m, data)
+        for p in range(m):
+            assert np.array_equal(enc[p], parity[p])
+
+
+def test_diff_update_lost_parity_and_overlap(gpu, oracle):
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    n = 4096
+    data = [oracle.splitmix_bytes(10 + j, 4 * n) for j in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    new = oracle.splitmix_bytes(99, n)
+    ddev = [to_dev(torch, d) for d in data]
+    p0 = to_dev(torch, parity[0])
+    with ec.Plan([(n, 0, n, 1)]) as plan:
+        ec.diff_update(k, m, mat, ddev, to_dev(torch, new), [p0, None], True, plan)
+        torch.cuda.synchronize()
+    old = data[1][n:2 * n].copy()
+    pv = [parity[0][n:2 * n].copy(), np.zeros(n, np.uint8)]
+    oracle.diff_update(mat, k, m, 1, old, new, pv, True)
+    parity[0][n:2 * n] = pv[0]
+    data[1][n:2 * n] = old
+    assert np.array_equal(to_host(p0), parity[0])
+    assert np.array_equal(to_host(ddev[1]), data[1])
+    with ec.Plan([(0, 0, 4096, 0), (4000, 0, 200, 1)]) as plan:  # overlapping SETs
+        with pytest.raises(ec.CecError) as ei:
+            ec.diff_update(k, m, mat, ddev, to_dev(torch, new), [p0, None], True, plan)
+        assert ei.value.code == ec.CEC_EOVERLAP
+
+
+def test_set_diff_and_apply_diffs(gpu, oracle, engine):
+    torch, ec = gpu
+    k, m = 4, 2
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(5)
+    lens = [int(x) for x in rng.integers(1, 9000, 30)]
+    ext, arena_len, stage_len = make_extents(rng, lens, unaligned_every=6)
+    for e in ext:
+        e[3] = int(rng.integers(0, k))
+    data = [rng.integers(0, 256, arena_len, dtype=np.uint8) for _ in range(k)]
+    staging = rng.integers(0, 256, stage_len, dtype=np.uint8)
+    diff_dev = to_dev(torch, np.zeros(stage_len, np.uint8))
+    par = rng.integers(0, 256, arena_len, dtype=np.uint8)
+    par_dev = to_dev(torch, par)
+    with ec.Plan([tuple(e) for e in ext]) as plan:
+        ec.set_diff(k, [to_dev(torch, d) for d in data], to_dev(torch, staging), diff_dev, plan)
+        ec.apply_diffs(k, m, mat, k + 1, diff_dev, par_dev, plan)
+        torch.cuda.synchronize()
+    diffs = to_host(diff_dev)
+    for off, soff, n, j in ext:
+        d = oracle.set_diff(data[j][off:off + n].copy(), staging[soff:soff + n].copy())
+        assert np.array_equal(diffs[soff:soff + n], d)
+        pv = par[off:off + n].copy()
+        oracle.parity_apply(mat, k, k + 1, j, d, pv)
+        par[off:off + n] = pv
+    assert np.array_equal(to_host(par_dev), par)
+
+
+# ------------------------------------------------------------------ recovery (a6, a7)
+def all_masks(k, m):
+    for lids in itertools.combinations(range(k + m), k):
+        mask = sum(1 << x for x in lids)
+        if mask != (1 << k) - 1:
+            yield mask
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3), (4, 4)])
+def test_decode_every_mask(gpu, oracle, engine, k, m):
+    torch, ec = gpu
+    mat = ec.coding_matrix(k, m)
+    masks = list(all_masks(k, m))
+    rng = np.random.default_rng(31 * k + m)
+    lens = [4096] * 8 + [1, 17, 4098, 65536 + 5, 300]
+    ext, arena_len, _ = make_extents(rng, lens * 3, unaligned_every=9)
+    for e in ext:
+        e[3] = int(rng.integers(0, len(masks)))
+    data = [rng.integers(0, 256, arena_len, dtype=np.uint8) for _ in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    arenas = data + parity
+    adev = [to_dev(torch, a) for a in arenas]
+    out0 = np.full(arena_len, SENT, np.uint8)
+    odev = [to_dev(torch, out0) for _ in range(k)]
+    with ec.Plan([tuple(e) for e in ext]) as plan:
+        ec.decode(k, m, mat, masks, adev, odev, plan)
+        torch.cuda.synchronize()
+    exp = [out0.copy() for _ in range(k)]
+    for off, _, n, q in ext:
+        mask = masks[q]
+        lost = [j for j in range(k) if not (mask >> j) & 1]
+        ref = oracle.decode(mat, k, m, mask, [a[off:off + n].copy() if (mask >> i) & 1 else None
+                                              for i, a in enumerate(arenas)])
+        for x, j in enumerate(lost):
+            assert np.array_equal(ref[x], data[j][off:off + n])  # oracle round trip
+            exp[j][off:off + n] = ref[x]
+    for j in range(k):
+        assert np.array_equal(to_host(odev[j]), exp[j]), f"rebuilt shard {j}"
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3)])
+def test_residual_then_solve(gpu, oracle, engine, k, m):
+    torch, ec = gpu
+    mat = ec.coding_matrix(k, m)
+    n = 64 * 4096  # 64 recovery units
+    data = [oracle.splitmix_bytes(0xC0C70005 + j, n) for j in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    arenas = data + parity
+    adev = [to_dev(torch, a) for a in arenas]
+    for mask in all_masks(k, m):
+        pars = [p for p in range(k, k + m) if (mask >> p) & 1]
+        lost = [j for j in range(k) if not (mask >> j) & 1]
+        res = {p: to_dev(torch, np.zeros(n, np.uint8)) for p in pars}
+        outs = {j: to_dev(torch, np.zeros(n, np.uint8)) for j in lost}
+        with ec.Plan([(0, 0, n, 0)]) as plan:
+            for p in pars:
+                ec.residual(k, m, mat, p, mask, adev, res[p], plan)
+            ec.solve(k, m, mat, mask, [res.get(i) for i in range(k + m)],
+                     [outs.get(j) for j in range(k)], plan)
+            torch.cuda.synchronize()
+        C = []
+        for p in pars:  # recovery_recover_units, survivor by survivor
+            r = np.empty(n, np.uint8)
+            touched = [0]
+            for s in range(k):
+                if (mask >> s) & 1:
+                    oracle.recover_units(mat, k, p, s, parity[p - k], data[s], r, touched)
+            if not touched[0]:
+                r[:] = parity[p - k]
+            assert np.array_equal(to_host(res[p]), r), (hex(mask), p)
+            C.append(r)
+        ref = oracle.bottom_half(mat, k, m, mask, C)
+        for x, j in enumerate(lost):
+            assert np.array_equal(ref[x], data[j])
+            assert np.array_equal(to_host(outs[j]), data[j]), (hex(mask), j)
+
+
+def test_recovery_mask_matches_reference(gpu, oracle):
+    _, ec = gpu
+    rng = np.random.default_rng(3)
+    for _ in range(200):
+        k, m = int(rng.integers(1, 9)), int(rng.integers(1, 5))
+        conn = [int(x) for x in rng.integers(0, 2, k + m)]
+        leader = int(rng.integers(k, k + m))
+        assert ec.recovery_mask(k, m, leader, conn) == oracle.recovery_mask(k, m, leader, conn)
+
+
+# ------------------------------------------------------------------ BASELINE full sizes
+def test_cfg2_full_size_roundtrip(gpu, oracle):
+    """BASELINE configs[1]: RS(3,2), 65,536 x 4 KiB stripes; encode, erase one data
+    shard per stripe (leader rotates over both parities), decode; compare on device."""
+    torch, ec = gpu
+    k, m, n, B = 3, 2, 4096, 65536
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70002)
+    data = [torch.randint(0, 256, (B * n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    # lost data shard j, leader parity k+p (start_recovery, memcached.c:8136-8151)
+    masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
+             for p in range(m) for j in range(k)]
+    assert all(masks) and len(set(masks)) == k * m
+    with ec.Plan([(s * n, 0, n, 0) for s in range(B)]) as enc_plan, \
+         ec.Plan([(s * n, 0, n, s % len(masks)) for s in range(B)]) as dec_plan:
+        ec.encode(k, m, mat, data, parity, enc_plan)
+        ec.decode(k, m, mat, masks, data + parity, out, dec_plan)
+        torch.cuda.synchronize()
+    lost_of = [[j for j in range(k) if not (mk >> j) & 1][0] for mk in masks]
+    for q, j in enumerate(lost_of):
+        sel = torch.arange(q, B, len(masks), device="cuda")
+        got = out[j].view(B, n)[sel]
+        want = data[j].view(B, n)[sel]
+        assert torch.equal(got, want), f"mask {q}"
+    for s in [0, 1, 4097, B - 1]:  # spot-check parity against the oracle
+        d = [to_host(x[s * n:(s + 1) * n]) for x in data]
+        ps = oracle.encode(mat, k, m, d)
+        for p in range(m):
+            assert np.array_equal(to_host(parity[p][s * n:(s + 1) * n]), ps[p])
+
+
+def test_cfg5_1mib_decode_d0_p0_and_d1_p1(gpu, oracle):
+    """BASELINE configs[4]: RS(3,2) online recovery of one lost data shard, 1 MiB values
+    x 1,024: D0 with leader P0 (inverse 1) and D1 with leader P1 (inverse 1/245)."""
+    torch, ec = gpu
+    k, m, n, B = 3, 2, 1 << 20, 1024
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70005)
+    data = [torch.randint(0, 256, (B * n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, parity, B * n)
+    m_d0 = ec.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])  # D0 lost, leader P0
+    m_d1 = ec.recovery_mask(k, m, 4, [1, 0, 1, 0, 1])  # D1 + P0 lost, leader P1
+    assert (m_d0, m_d1) == (0b01110, 0b10101)
+    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    with ec.Plan([(s * n, 0, n, s & 1) for s in range(B)]) as plan:
+        ec.decode(k, m, mat, [m_d0, m_d1], data + parity, out, plan)
+        torch.cuda.synchronize()
+    assert torch.equal(out[0].view(B, n)[0::2], data[0].view(B, n)[0::2])
+    assert torch.equal(out[1].view(B, n)[1::2], data[1].view(B, n)[1::2])
+    assert int(out[2].count_nonzero()) == 0
+    s = 1  # one stripe through the reference chain
+    arenas = [to_host(x[s * n:(s + 1) * n]) for x in data + parity]
+    ref = oracle.decode(mat, k, m, m_d1, [a if (m_d1 >> i) & 1 else None for i, a in enumerate(arenas)])
+    assert np.array_equal(ref[0], to_host(out[1][s * n:(s + 1) * n]))
+
+
+def test_cfg4_rs42_64k_roundtrip(gpu, oracle):
+    """BASELINE configs[3] (per GPU): RS(4,2), 64 KiB values x 16,384 stripes."""
+    torch, ec = gpu
+    k, m, n, B = 4, 2, 65536, 16384
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70004)
+    data = [torch.randint(0, 256, (B * n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    with ec.Plan([(s * n, 0, n, 0) for s in range(B)]) as plan:
+        ec.encode(k, m, mat, data, parity, plan)
+        torch.cuda.synchronize()
+    # double erasure (D0, D3) from both parities, in place of the lost arenas
+    mask = 0b110110
+    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    with ec.Plan([(0, 0, B * n // 2, 0), (B * n // 2, 0, B * n // 2, 0)]) as plan:
+        ec.decode(k, m, mat, [mask], data + parity, out, plan)
+        torch.cuda.synchronize()
+    assert torch.equal(out[0], data[0]) and torch.equal(out[3], data[3])
+    s = 12345
+    d = [to_host(x[s * n:(s + 1) * n]) for x in data]
+    ps = oracle.encode(mat, k, m, d)
+    for p in range(m):
+        assert np.array_equal(to_host(parity[p][s * n:(s + 1) * n]), ps[p])
+
+
+# ------------------------------------------------------------------ the drop-in symbols
+def test_dropin_host_buffers(gpu, oracle):
+    """galois_w08_region_multiply on pageable host memory at arbitrary alignment."""
+    _, ec = gpu
+    rng = np.random.default_rng(11)
+    for n in [1, 2, 4095, 4098, 65537, 3 << 20]:
+        for so, do in [(0, 0), (5, 9), (16, 3)]:
+            for c in [1, 2, 245, 0]:
+                buf = rng.integers(0, 256, n + 32, dtype=np.uint8)
+                dst = rng.integers(0, 256, n + 32, dtype=np.uint8)
+                exp = dst.copy()
+                v = exp[do:do + n].copy()
+                oracle.region_multiply(buf[so:so + n].copy(), c, v, 1)
+                exp[do:do + n] = v
+                ec.galois_w08_region_multiply(buf[so:], c, n, dst[do:], 1)
+                assert np.array_equal(dst, exp), (n, so, do, c)
+
+
+def test_dropin_device_buffers(gpu, oracle):
+    torch, ec = gpu
+    a = oracle.splitmix_bytes(1, 10000)
+    b = oracle.splitmix_bytes(2, 10000)
+    exp = b.copy()
+    oracle.region_multiply(a, 0x8E, exp, 1)
+    da, db = to_dev(torch, a), to_dev(torch, b)
+    ec.galois_w08_region_multiply(da, 0x8E, 10000, db, 1)
+    assert np.array_equal(to_host(db), exp)
+
+
+def test_dropin_c_program(gpu, oracle, tmp_path):
+    """A C program written against include/{galois,jerasure,reed_sol}.h and linked with
+    -lJerasure (the shim) replays the reference's call chain; outputs vs the oracle."""
+    from tests.dropin import run_dropin_case
+
+    run_dropin_case(oracle, tmp_path)
