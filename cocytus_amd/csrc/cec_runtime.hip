@@ -33,7 +33,7 @@
 
 using namespace cec;
 
-static_assert(sizeof(Extent) == sizeof(cec_extent), "extent layout");
+static_assert(sizeof(Tile) == sizeof(cec_extent), "tile layout");
 static_assert(CEC_MAX_K <= kPatN, "k capacity");
 
 // ============================================================== errors
@@ -217,10 +217,9 @@ struct cec_plan {
     int64_t n_tiles = 0;
     uint64_t total = 0;
     bool overlap = false;
-    Extent *d_ext = nullptr;
-    TileEnt *d_tiles = nullptr;
-    std::vector<cec_extent> h_ext;  // kept alive for the async upload
-    std::vector<TileEnt> h_tiles;
+    Tile *d_tiles = nullptr;
+    std::vector<cec_extent> h_ext;  // validation of per-op pattern indices
+    std::vector<Tile> h_tiles;      // kept alive for the async upload
 };
 
 CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *stream) {
@@ -236,7 +235,9 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
     for (int e = 0; e < n; ++e) {
         const uint32_t len = ext[e].len;
         p->total += len;
-        for (uint32_t o = 0; o < len; o += kTile) p->h_tiles.push_back(TileEnt{static_cast<uint32_t>(e), o});
+        for (uint32_t o = 0; o < len; o += kTile)
+            p->h_tiles.push_back(Tile{ext[e].off + o, ext[e].src_off + o,
+                                      std::min<uint32_t>(kTile, len - o), ext[e].pattern});
     }
     if (p->h_tiles.size() > 0xFFFFFFFFull) {
         delete p;
@@ -253,22 +254,17 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
             if (r[i].first < r[i - 1].second) { p->overlap = true; break; }
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
-    if (n > 0) {
-        if (hipMalloc(&p->d_ext, sizeof(Extent) * n) != hipSuccess) {
-            delete p;
-            return fail(CEC_ENOMEM, "cec_plan_create: hipMalloc extents");
-        }
-        HIP_TRY(hipMemcpyAsync(p->d_ext, p->h_ext.data(), sizeof(Extent) * n,
-                               hipMemcpyHostToDevice, s));
-    }
     if (p->n_tiles > 0) {
-        if (hipMalloc(&p->d_tiles, sizeof(TileEnt) * p->n_tiles) != hipSuccess) {
-            (void)hipFree(p->d_ext);
+        if (hipMalloc(&p->d_tiles, sizeof(Tile) * p->n_tiles) != hipSuccess) {
             delete p;
             return fail(CEC_ENOMEM, "cec_plan_create: hipMalloc tiles");
         }
-        HIP_TRY(hipMemcpyAsync(p->d_tiles, p->h_tiles.data(), sizeof(TileEnt) * p->n_tiles,
-                               hipMemcpyHostToDevice, s));
+        if (hipMemcpyAsync(p->d_tiles, p->h_tiles.data(), sizeof(Tile) * p->n_tiles,
+                           hipMemcpyHostToDevice, s) != hipSuccess) {
+            (void)hipFree(p->d_tiles);
+            delete p;
+            return fail(CEC_EHIP, "cec_plan_create: tile upload failed");
+        }
     }
     *out = p;
     return CEC_OK;
@@ -278,7 +274,6 @@ CEC_API int cec_plan_destroy(cec_plan *p) {
     if (!p) return CEC_OK;
     int rc = CEC_OK;
     if (hipDeviceSynchronize() != hipSuccess) rc = fail(CEC_EHIP, "hipDeviceSynchronize");
-    if (p->d_ext) (void)hipFree(p->d_ext);
     if (p->d_tiles) (void)hipFree(p->d_tiles);
     delete p;
     return rc;
@@ -297,7 +292,6 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     if (plan) {
         if (plan->device != dev)
             return fail(CEC_EINVAL, "plan built on device %d used on device %d", plan->device, dev);
-        a.extents = plan->d_ext;
         a.tiles = plan->d_tiles;
         n_tiles = static_cast<uint64_t>(plan->n_tiles);
     } else {
@@ -316,10 +310,14 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     if (int r = upload_patterns(dev, pats, &dp)) return r;
     a.patterns = dp;
     a.n_tiles = static_cast<uint32_t>(n_tiles);
-    const uint64_t max_grid = static_cast<uint64_t>(g_dev[dev].cus) * 8;
+    // PERM: one workgroup per tile, dispatched in tile order, so the set of tiles in
+    // flight is a contiguous window of the arenas (measured 5-12 % over a persistent
+    // grid-stride grid: DESIGN.md).  LDS: persistent grid, so the per-workgroup
+    // table staging is amortised over many tiles.
+    const bool lds = g_engine.load() == CEC_ENGINE_LDS;
+    const uint64_t max_grid = lds ? static_cast<uint64_t>(g_dev[dev].cus) * 8 : 0x7FFFFFFFull;
     const int grid = static_cast<int>(std::min<uint64_t>(n_tiles, max_grid));
     int en, el, eacc;
-    const bool lds = g_engine.load() == CEC_ENGINE_LDS;
     const bool exact = exact_shape(pats, &en, &el, &eacc) &&
                        (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, stream)
                             : launch_exact<PermEngine>(en, el, eacc, a, grid, stream));
