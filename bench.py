@@ -3,23 +3,29 @@
 
 Metric (BASELINE.json): GiB/s device-resident RS(3,2) encode+decode, 4 KiB values.
 One step = one batch of the workload on each GPU, inputs already resident in HBM:
-  1. cec_encode  over B stripes  (parity[p] = sum_j MATRIX(K+p, j) * D_j, per 4 KiB value)
-  2. cec_decode  over the same B stripes, one lost data shard per stripe, the lost shard
-     and the recovery leader rotating over all K x M (lost shard, leader parity) pairs
-     (masks as start_recovery builds them, memcached.c:8136-8151).
-value = payload GiB/s over all ranks = (K*n encoded + n rebuilt) * B * N * steps / max-rank
-time / 2^30.  roofline = the encode kernel's algorithmic HBM bytes ((K+M)*n per stripe)
-per launch / its HIP-event launch time, against 8 TB/s.  cpu_baseline = the oracle's
-restated Jerasure/GF-Complete path (AVX2 split-nibble) on the host, same chaining.
+  1. cec_encode  over B stripes  (parity[p] = sum_j MATRIX(K+p, j) * D_j, per value)
+  2. cec_decode  over the same B stripes, one lost data shard per stripe; the lost shard
+     and the recovery leader rotate over all K x M (lost shard, leader parity) pairs
+     (masks as start_recovery builds them, /root/reference/memcached.c:8136-8151).
+value = payload GiB/s over all ranks = (K*n encoded + n rebuilt) per stripe * stripes *
+ranks * steps / max-over-ranks wall time / 2^30.  roofline = the encode kernel's
+algorithmic HBM bytes ((K+M)*n per stripe) per launch / its HIP-event launch time vs
+8 TB/s; traffic = HBM bytes per launch from the committed rocprofv3 --pmc summary.
+cpu_baseline = the oracle's restated Jerasure/GF-Complete path (AVX2 split-nibble), on
+the host cores, same chaining as the reference's call sites.
 
-Multi-GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N`; each rank
+Multi-GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N`: every rank
 encodes/decodes its own batch (independent stripes, no collective on the data path);
-barrier + synchronize around the timed steps, max over ranks.
+barrier + synchronize around the timed steps, max over ranks (weak scaling).
+
+--e2e: values start and end in pinned host memory (client sockets / recovery peers):
+H2D -> kernel -> D2H pipelined over 3 HIP streams; printed as its own JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import sys
 import time
@@ -27,27 +33,62 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+METRIC = "GiB/s device-resident RS(3,2) encode+decode, 4 KiB values"
 
 WORKLOADS = {
-    # name: (k, m, value bytes, stripes per GPU)
-    "rs32_4k": (3, 2, 4096, 65536),        # BASELINE configs[1] (+ decode: the metric)
-    "rs32_1m": (3, 2, 1 << 20, 1024),      # configs[4] sizes
-    "rs42_64k": (4, 2, 65536, 16384),      # configs[3] per GPU
+    # name: (k, m, value bytes (0 = mixed), stripes per GPU, what)
+    "rs32_4k": (3, 2, 4096, 65536, "BASELINE configs[1] (+ decode): the metric"),
+    "rs32_mixed": (3, 2, 0, 0, "BASELINE configs[2]: log-uniform 256 B - 1 MiB values, ~1 GiB"),
+    "rs42_64k": (4, 2, 65536, 16384, "BASELINE configs[3], per GPU"),
+    "rs32_1m": (3, 2, 1 << 20, 1024, "BASELINE configs[4] sizes"),
 }
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
     ap.add_argument("--engine", default="perm", choices=["perm", "lds"])
+    ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU work budget (thread-seconds)")
-    ap.add_argument("--quiet", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def layout(workload, seed=0xC0C70003):
+    """[(arena offset, length)] of every stripe; starts 16-B aligned (ecalloc.c:176)."""
+    k, m, n, B, _ = WORKLOADS[workload]
+    if n:
+        return [(s * n, n) for s in range(B)], B * n
+    import random
+
+    rng = random.Random(seed)
+    out, off, total = [], 0, 0
+    lo, hi = math.log(256), math.log(1 << 20)
+    while total < (1 << 30):
+        ln = int(math.exp(rng.uniform(lo, hi)))
+        out.append((off, ln))
+        total += ln
+        off = (off + ln + 15) & ~15
+    return out, off
+
+
+def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous split of `total` units over `world` ranks."""
+    return total * rank // world, total * (rank + 1) // world
+
+
+def max_over_ranks(values, dist, device):
+    """Element-wise max of a list of floats over all ranks (identity when alone)."""
+    import torch
+
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(x) for x in t.tolist()]
 
 
 def cpu_baseline(k, m, n, budget_s):
@@ -56,12 +97,9 @@ def cpu_baseline(k, m, n, budget_s):
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
-    stripes = 16384  # 64 MiB per shard at 4 KiB: larger than the host LLC
-    if n * stripes > (256 << 20):
-        stripes = max(threads, (256 << 20) // n)
+    stripes = max(threads, (64 << 20) // n)  # 64 MiB per shard: larger than the host LLC
     t1 = pyoracle.bench_encode_decode(k, m, n, stripes, threads, 1, True)
-    reps = max(1, int(budget_s / max(t1 * threads, 1e-6)))
-    reps = min(reps, 50)
+    reps = max(1, min(200, int(budget_s / max(t1 * threads, 1e-6))))
     t = pyoracle.bench_encode_decode(k, m, n, stripes, threads, reps, True)
     payload = (k + 1) * n * stripes * reps
     return {
@@ -69,74 +107,76 @@ def cpu_baseline(k, m, n, budget_s):
         "unit": "GiB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes x {reps} passes, "
-                  f"{threads} threads, {t:.2f} s wall; restated GF-Complete SPLIT(8,4) "
-                  f"split-nibble ({'AVX2' if pyoracle.simd_available() else 'scalar'}), "
+        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes x {reps} passes on "
+                  f"{threads} threads ({t:.2f} s wall, {t * threads:.1f} thread-s); restated "
+                  f"GF-Complete SPLIT(8,4) split-nibble ({'AVX2' if pyoracle.simd_available() else 'scalar'}), "
                   "chained like memcached.c/recovery.c (Jerasure not available)",
     }
 
 
 def load_traffic(workload):
-    """HBM bytes per encode launch from the committed rocprofv3 --pmc summary."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/)."""
     try:
-        with open(p) as f:
-            d = json.load(f)
-        e = d.get(workload, {})
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            e = json.load(f).get(workload, {})
         return e.get("encode_hbm_bytes_per_launch"), e.get("decode_hbm_bytes_per_launch")
     except (OSError, ValueError):
         return None, None
 
 
-def main():
-    args = parse()
+def setup():
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run")
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.empty(1, device="cuda")
-
+    torch.empty(1, device="cuda")  # torch owns the HIP runtime before the library loads
     from cocytus_amd import ec
 
     ec.lib()
     if ec.device_check() != ec.CEC_OK:
         raise SystemExit("libcocytus_ec: " + ec.lib().cec_last_error().decode())
-    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+    return torch, dist, ec, world, rank
 
-    k, m, n, B = WORKLOADS[args.workload]
+
+def run_device(args):
+    torch, dist, ec, world, rank = setup()
+    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+    k, m, n, _, what = WORKLOADS[args.workload]
+    stripes, arena = layout(args.workload)
+    B = len(stripes)
     mat = ec.coding_matrix(k, m)
     g = torch.Generator(device="cuda").manual_seed(0xC0C70002 + rank)
-    data = [torch.randint(0, 256, (B * n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
-    parity = [torch.empty(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
-    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    data = [torch.randint(0, 256, (arena,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(arena, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    out = [torch.zeros(arena, dtype=torch.uint8, device="cuda") for _ in range(k)]
     masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
              for p in range(m) for j in range(k)]
-    enc_plan = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
-    dec_plan = ec.Plan([(s * n, 0, n, s % len(masks)) for s in range(B)])
+    enc_plan = ec.Plan([(o, 0, ln, 0) for o, ln in stripes])
+    dec_plan = ec.Plan([(o, 0, ln, s % len(masks)) for s, (o, ln) in enumerate(stripes)])
     stream = torch.cuda.current_stream()
-
-    def step():
-        ec.encode(k, m, mat, data, parity, enc_plan, stream)
-        ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
+    bytes_total = sum(ln for _, ln in stripes)
 
     for _ in range(args.warmup):
-        step()
+        ec.encode(k, m, mat, data, parity, enc_plan, stream)
+        ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
     torch.cuda.synchronize()
 
-    # verify once (device-side): every rebuilt shard equals the original
-    ok = True
-    for q, mk in enumerate(masks):
-        j = [x for x in range(k) if not (mk >> x) & 1][0]
-        sel = torch.arange(q, B, len(masks), device="cuda")
-        ok &= bool(torch.equal(out[j].view(B, n)[sel], data[j].view(B, n)[sel]))
+    import numpy as np
+
+    ok = True  # every rebuilt shard equals the original (compared on the device)
+    lost_of = [[x for x in range(k) if not (mk >> x) & 1][0] for mk in masks]
+    for j in range(k):
+        sel = np.zeros(arena, dtype=bool)
+        for s, (o, ln) in enumerate(stripes):
+            if lost_of[s % len(masks)] == j:
+                sel[o:o + ln] = True
+        sel_d = torch.from_numpy(sel).cuda()
+        ok &= bool(torch.equal(out[j][sel_d], data[j][sel_d]))
 
     evs = [[ec.Event() for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
@@ -155,23 +195,18 @@ def main():
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_ms(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_ms(e[2]) for e in evs) / args.steps
+    elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist, "cuda")
 
-    t = torch.tensor([elapsed, enc_ms, dec_ms, 0.0 if ok else 1.0], dtype=torch.float64, device="cuda")
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, enc_ms_max, dec_ms_max, bad = [float(x) for x in t.tolist()]
-
-    payload = (k * n + n) * B * world * args.steps
+    payload = (k + 1) * bytes_total * world * args.steps
     value = payload / elapsed / 2**30
-    enc_bytes = (k + m) * n * B          # algorithmic HBM bytes per encode launch
-    dec_bytes = (k + 1) * n * B          # per decode launch (read K survivors, write 1)
+    enc_bytes = (k + m) * bytes_total  # algorithmic HBM bytes per encode launch
+    dec_bytes = (k + 1) * bytes_total  # per decode launch (read K survivors, write 1)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
     enc_traffic, dec_traffic = load_traffic(args.workload)
-
     if rank == 0:
         res = {
-            "metric": "GiB/s device-resident RS(3,2) encode+decode, 4 KiB values",
+            "metric": METRIC if args.workload == "rs32_4k" else f"GiB/s device-resident {args.workload}",
             "value": round(value, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -184,10 +219,11 @@ def main():
             "dtype": "u8",
             "data": "synthetic (uniform random bytes, torch.Generator seeded per rank)",
             "config": {
-                "workload": f"RS({k},{m}) encode + single-shard decode, {n} B values, "
-                            f"{B} stripes per GPU (BASELINE configs[1] + decode)",
-                "k": k, "m": m, "value_bytes": n, "stripes_per_gpu": B,
-                "parallelism": f"{world} independent shards of stripes, no collective",
+                "workload": f"RS({k},{m}) encode + single-shard decode, "
+                            f"{'%d B' % n if n else 'mixed 256 B-1 MiB'} values, {B} stripes per GPU ({what})",
+                "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
+                "bytes_per_shard_per_gpu": bytes_total,
+                "parallelism": f"{world} x independent stripe batches, no collective",
                 "engine": args.engine,
             },
             "roofline": {
@@ -197,7 +233,8 @@ def main():
                 "unit": "GB/s",
                 "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
                 "traffic": enc_traffic,
-                "kernel": "combine_kernel<3,2,PermEngine,kAccNone,exact> (cec_encode)",
+                "kernel": f"combine_kernel<{k},{m},{'PermEngine' if args.engine == 'perm' else 'LdsEngine'},"
+                          "kAccNone,exact> (cec_encode)",
                 "algorithmic_bytes_per_launch": enc_bytes,
                 "launch_ms": round(enc_ms, 4),
             },
@@ -209,11 +246,97 @@ def main():
             "verified": ok and bad == 0.0,
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(k, m, n, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(k, m, n or 4096, args.cpu_seconds)
         print(json.dumps(res), flush=True)
     enc_plan.destroy()
     dec_plan.destroy()
-    if world > 1:
+
+
+def run_e2e(args):
+    """Values start and end in pinned host memory: per chunk, H2D of the K data shards
+    -> encode -> D2H of the M parities, and H2D of the K survivors (D1..D_{K-1}, P0)
+    -> decode of D0 -> D2H of the rebuilt shard; chunks round-robin over 3 streams."""
+    torch, dist, ec, world, rank = setup()
+    k, m, n, B, _ = WORKLOADS["rs32_4k"]
+    mat = ec.coding_matrix(k, m)
+    chunk = 4096  # stripes per chunk: 16 MiB per shard
+    nch = B // chunk
+    clen = chunk * n
+    pin = dict(dtype=torch.uint8, pin_memory=True)
+    data_h = [torch.randint(0, 256, (B * n,), dtype=torch.uint8).pin_memory() for _ in range(k)]
+    par_h = [torch.empty(B * n, **pin) for _ in range(m)]
+    out_h = torch.empty(B * n, **pin)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    slots = [{"d": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(k)],
+              "p": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(m)],
+              "o": torch.empty(clen, dtype=torch.uint8, device="cuda")} for _ in streams]
+    mask = ec.recovery_mask(k, m, k, [0] + [1] * (k + m - 1))  # D0 lost, leader P0
+    plan = ec.Plan([(s * n, 0, n, 0) for s in range(chunk)])
+
+    def step():
+        for c in range(nch):
+            st, sl = streams[c % 3], slots[c % 3]
+            lo, hi = c * clen, (c + 1) * clen
+            with torch.cuda.stream(st):
+                for j in range(k):
+                    sl["d"][j].copy_(data_h[j][lo:hi], non_blocking=True)
+                ec.encode(k, m, mat, sl["d"], sl["p"], plan, st)
+                for p in range(m):
+                    par_h[p][lo:hi].copy_(sl["p"][p], non_blocking=True)
+                for j in range(1, k):  # survivors arrive again from the peers
+                    sl["d"][j].copy_(data_h[j][lo:hi], non_blocking=True)
+                sl["p"][0].copy_(par_h[0][lo:hi], non_blocking=True)
+                ec.decode(k, m, mat, [mask], sl["d"] + sl["p"], [sl["o"], None, None], plan, st)
+                out_h[lo:hi].copy_(sl["o"], non_blocking=True)
+
+    for _ in range(max(1, args.warmup)):
+        step()
+    torch.cuda.synchronize()
+    ok = torch.equal(out_h, data_h[0])
+    steps = max(1, min(args.steps, 10))
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    # raw copy rates for context
+    x = torch.empty(256 << 20, **pin)
+    y = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(4):
+        y.copy_(x, non_blocking=True)
+    torch.cuda.synchronize()
+    h2d = 4 * (256 << 20) / (time.perf_counter() - t1) / 1e9
+    t1 = time.perf_counter()
+    for _ in range(4):
+        x.copy_(y, non_blocking=True)
+    torch.cuda.synchronize()
+    d2h = 4 * (256 << 20) / (time.perf_counter() - t1) / 1e9
+    payload = (k + 1) * B * n * steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s end-to-end (pinned host -> HBM -> host) RS(3,2) encode+decode, 4 KiB values",
+            "value": round(payload / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+            "ms_per_step": round(el * 1e3 / steps, 3), "verified": bool(ok),
+            "h2d_bytes_per_stripe": (2 * k) * n, "d2h_bytes_per_stripe": (m + 1) * n,
+            "pcie_h2d_GBps_raw": round(h2d, 1), "pcie_d2h_GBps_raw": round(d2h, 1),
+            "config": {"chunk_stripes": chunk, "streams": 3, "stripes": B},
+        }), flush=True)
+    plan.destroy()
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
+    if args.e2e:
+        run_e2e(args)
+    else:
+        run_device(args)
+    import torch.distributed as dist
+
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -1,0 +1,22 @@
+#!/bin/bash
+# tools/profile_round.sh ROUND -- rocprofv3 evidence for the bench command (run ON the GPU box).
+#   pass 1: --kernel-trace --stats      (per-kernel average duration)
+#   pass 2: --pmc FETCH_SIZE            (HBM read bytes; separate pass: TCC slots)
+#   pass 3: --pmc WRITE_SIZE            (HBM write bytes)
+# then tools/pmc_summary.py writes profiles/ROUND_* and profiles/pmc_traffic.json.
+set -euo pipefail
+ROUND=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/prof_$ROUND
+mkdir -p "$OUT"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline"
+cd /tmp && export TMPDIR=/tmp
+for W in rs32_4k rs42_64k rs32_1m; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$W" -o run --output-format csv \
+      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_trace_$W.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch_$W" -o run --output-format csv \
+      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_fetch_$W.log" 2>&1
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write_$W" -o run --output-format csv \
+      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_write_$W.log" 2>&1
+done
+python3 "$R/tools/pmc_summary.py" "$OUT" "$ROUND"
