@@ -55,6 +55,8 @@ def parse(argv=None):
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU work budget (thread-seconds)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for the barrier / max-over-ranks (nccl = RCCL)")
     return ap.parse_args(argv)
 
 
@@ -81,13 +83,15 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return total * rank // world, total * (rank + 1) // world
 
 
-def max_over_ranks(values, dist, device):
+def max_over_ranks(values, dist):
     """Element-wise max of a list of floats over all ranks (identity when alone)."""
     import torch
 
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [float(x) for x in values]
+    device = "cuda" if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor(values, dtype=torch.float64, device=device)
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(x) for x in t.tolist()]
 
 
@@ -124,16 +128,22 @@ def load_traffic(workload):
         return None, None
 
 
-def setup():
+def setup(backend="nccl"):
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    # CEC_BENCH_DEVICE pins every rank to one device: a gloo rehearsal of the
+    # multi-rank path on a one-GPU box (never used for reported numbers).
+    dev = int(os.environ.get("CEC_BENCH_DEVICE", local))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group("gloo")
     torch.empty(1, device="cuda")  # torch owns the HIP runtime before the library loads
     from cocytus_amd import ec
 
@@ -144,7 +154,7 @@ def setup():
 
 
 def run_device(args):
-    torch, dist, ec, world, rank = setup()
+    torch, dist, ec, world, rank = setup(args.dist_backend)
     ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
     k, m, n, _, what = WORKLOADS[args.workload]
     stripes, arena = layout(args.workload)
@@ -195,7 +205,7 @@ def run_device(args):
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_ms(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_ms(e[2]) for e in evs) / args.steps
-    elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist, "cuda")
+    elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist)
 
     payload = (k + 1) * bytes_total * world * args.steps
     value = payload / elapsed / 2**30
@@ -256,7 +266,7 @@ def run_e2e(args):
     """Values start and end in pinned host memory: per chunk, H2D of the K data shards
     -> encode -> D2H of the M parities, and H2D of the K survivors (D1..D_{K-1}, P0)
     -> decode of D0 -> D2H of the rebuilt shard; chunks round-robin over 3 streams."""
-    torch, dist, ec, world, rank = setup()
+    torch, dist, ec, world, rank = setup(args.dist_backend)
     k, m, n, B, _ = WORKLOADS["rs32_4k"]
     mat = ec.coding_matrix(k, m)
     chunk = 4096  # stripes per chunk: 16 MiB per shard

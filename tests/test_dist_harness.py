@@ -1,0 +1,72 @@
+"""The multi-rank bench harness on CPU (gloo, world size 2): contiguous sharding of a
+fixed batch, max-over-ranks timing, and the workload layouts."""
+from __future__ import annotations
+
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+
+    lo, hi = bench.shard_range(65536, rank, world)
+    # each rank's "elapsed" differs; the harness must report the slowest
+    got = bench.max_over_ranks([0.5 + rank, 0.0 if rank else 1.0], dist)
+    dist.barrier()
+    q.put((rank, lo, hi, got))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_max_and_shards():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 32768), (32768, 65536)]
+    for r in res:
+        assert r[3] == [1.5, 1.0]  # max elapsed over ranks, any rank's failure flag
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 4, 8])
+def test_shard_range_partitions(world):
+    import bench
+
+    total = 65537
+    spans = [bench.shard_range(total, r, world) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    for a, b in zip(spans, spans[1:]):
+        assert a[1] == b[0]
+    sizes = [hi - lo for lo, hi in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_layouts():
+    import bench
+
+    s, arena = bench.layout("rs32_4k")
+    assert len(s) == 65536 and arena == 65536 * 4096 and s[1] == (4096, 4096)
+    s, arena = bench.layout("rs32_mixed")
+    assert sum(ln for _, ln in s) >= 1 << 30
+    assert all(o % 16 == 0 for o, _ in s)  # ecalloc.c:176
+    assert all(256 <= ln <= 1 << 20 for _, ln in s)
+    assert all(a[0] + a[1] <= b[0] for a, b in zip(s, s[1:]))  # no overlap
+    assert bench.layout("rs32_mixed") == (s, arena)  # seeded
