@@ -188,34 +188,60 @@ __device__ inline TileRef load_tile(const CombineArgs &a, uint32_t t) {
     return r;
 }
 
-// Byte-granular body for ragged tails and misaligned tiles: bytes b of the tile,
-// b = first, first + step, ... < len.
+// A ragged chunk: the first cnt (1..16) bytes at base+off.  Branch-free: byte b
+// reads address off + min(b, cnt-1), so all 16 loads are in bounds and in flight
+// together (one memory latency, not sixteen dependent ones); bytes >= cnt read 0.
+__device__ inline uint4 gather16(const uint8_t *base, uint32_t off, uint32_t cnt) {
+    uint32_t v[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) v[b] = ld8(base, off + min(static_cast<uint32_t>(b), cnt - 1));
+    uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) w[b >> 2] |= (static_cast<uint32_t>(b) < cnt ? v[b] : 0u) << (8 * (b & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Store the first cnt bytes of v at base+off.  Byte b goes to off + min(b, cnt-1)
+// with the value of that clamped byte, so surplus stores rewrite the last valid byte
+// with its own (correct) value: no predication, never out of bounds.
+__device__ inline void scatter16(uint8_t *base, uint32_t off, uint32_t cnt, const uint4 &v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+        const uint32_t q = min(static_cast<uint32_t>(b), cnt - 1);
+        st8(base, off + q, w[q >> 2] >> (8 * (q & 3)));
+    }
+}
+
+// acc[l] ^= sum_i coef[l][i] * x[i] on one 16-byte chunk of every stream.
 template <int NT, int LT, class Eng>
-__device__ inline void combine_bytes(const CEC_CONST Pattern *P, const uint8_t *const *in,
-                                           uint8_t *const *out, int n_in, int n_out,
-                                           uint32_t first, uint32_t step, uint32_t len,
-                                           const uint32_t *lds) {
-    for (uint32_t b = first; b < len; b += step) {
-        uint32_t acc[LT];
+__device__ inline void compute_chunk(const CEC_CONST Pattern *P, int n_in, int n_out,
+                                     const uint4 (&x)[NT], uint4 (&acc)[LT], const uint32_t *lds) {
 #pragma unroll
-        for (int l = 0; l < LT; ++l)
-            acc[l] = (l < n_out && P->out_mode[l] == kModeXor) ? ld8(out[l], b) : 0u;
+    for (int i = 0; i < NT; ++i) {
+        if (i >= n_in) continue;
+        const uint32_t xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+        typename Eng::Sel s[4];
 #pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            if (i >= n_in) continue;
-            const uint32_t xb = ld8(in[i], b);
-            const typename Eng::Sel s = Eng::sel(xb, lds);
+        for (int w = 0; w < 4; ++w) s[w] = Eng::sel(xv[w], lds);
 #pragma unroll
-            for (int l = 0; l < LT; ++l) {
-                if (l >= n_out) continue;
-                const int c = P->coef[l][i];
-                if (c == 0) continue;
-                acc[l] ^= (c == 1) ? xb : (Eng::mul(s, P->tab[l][i], lds) & 0xFFu);
+        for (int l = 0; l < LT; ++l) {
+            if (l >= n_out) continue;
+            const int c = P->coef[l][i];
+            if (c == 0) continue;
+            if (c == 1) {
+                acc[l].x ^= xv[0];
+                acc[l].y ^= xv[1];
+                acc[l].z ^= xv[2];
+                acc[l].w ^= xv[3];
+            } else {
+                const CEC_CONST uint32_t *tb = P->tab[l][i];
+                acc[l].x ^= Eng::mul(s[0], tb, lds);
+                acc[l].y ^= Eng::mul(s[1], tb, lds);
+                acc[l].z ^= Eng::mul(s[2], tb, lds);
+                acc[l].w ^= Eng::mul(s[3], tb, lds);
             }
         }
-#pragma unroll
-        for (int l = 0; l < LT; ++l)
-            if (l < n_out) st8(out[l], b, acc[l]);
     }
 }
 
@@ -266,56 +292,44 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
             }
         }
 
-        if ((mis & 15) != 0) {
-            // misaligned tile (arbitrary device pointers): byte path, coalesced bytes
-            combine_bytes<NT, LT, Eng>(P, in, out, n_in, n_out, lane, kBlock, tr.len, lds);
-            continue;
-        }
+        // one 16-byte chunk per lane; the value's ragged tail (len = vlen + 2 is
+        // rarely a multiple of 16) and tiles of misaligned device pointers use the
+        // branch-free byte gather / scatter, everything else dwordx4.
         const uint32_t pos = lane * 16;
-        if (pos + 16 > tr.len) {
-            // ragged tail of the value (len = vlen + 2 is rarely a multiple of 16)
-            if (pos < tr.len) combine_bytes<NT, LT, Eng>(P, in, out, n_in, n_out, pos, 1, tr.len, lds);
-            continue;
-        }
+        if (pos >= tr.len) continue;
+        const uint32_t cnt = min(16u, tr.len - pos);
+        const bool wide = (mis & 15) == 0 && cnt == 16;
         uint4 x[NT];
         uint4 acc[LT];
+        if (wide) {
 #pragma unroll
-        for (int i = 0; i < NT; ++i)
-            if (i < n_in) x[i] = ld16(in[i], pos);
-#pragma unroll
-        for (int l = 0; l < LT; ++l) {
-            acc[l] = make_uint4(0, 0, 0, 0);
-            if (l < n_out && is_acc(l)) acc[l] = ld16(out[l], pos);
-        }
-#pragma unroll
-        for (int i = 0; i < NT; ++i) {
-            if (i >= n_in) continue;
-            const uint32_t xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
-            typename Eng::Sel s[4];
-#pragma unroll
-            for (int w = 0; w < 4; ++w) s[w] = Eng::sel(xv[w], lds);
+            for (int i = 0; i < NT; ++i)
+                if (i < n_in) x[i] = ld16(in[i], pos);
 #pragma unroll
             for (int l = 0; l < LT; ++l) {
-                if (l >= n_out) continue;
-                const int c = P->coef[l][i];
-                if (c == 0) continue;
-                if (c == 1) {
-                    acc[l].x ^= xv[0];
-                    acc[l].y ^= xv[1];
-                    acc[l].z ^= xv[2];
-                    acc[l].w ^= xv[3];
-                } else {
-                    const CEC_CONST uint32_t *tb = P->tab[l][i];
-                    acc[l].x ^= Eng::mul(s[0], tb, lds);
-                    acc[l].y ^= Eng::mul(s[1], tb, lds);
-                    acc[l].z ^= Eng::mul(s[2], tb, lds);
-                    acc[l].w ^= Eng::mul(s[3], tb, lds);
-                }
+                acc[l] = make_uint4(0, 0, 0, 0);
+                if (l < n_out && is_acc(l)) acc[l] = ld16(out[l], pos);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NT; ++i)
+                if (i < n_in) x[i] = gather16(in[i], pos, cnt);
+#pragma unroll
+            for (int l = 0; l < LT; ++l) {
+                acc[l] = make_uint4(0, 0, 0, 0);
+                if (l < n_out && is_acc(l)) acc[l] = gather16(out[l], pos, cnt);
             }
         }
+        compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
+        if (wide) {
 #pragma unroll
-        for (int l = 0; l < LT; ++l)
-            if (l < n_out) st16(out[l], pos, acc[l]);
+            for (int l = 0; l < LT; ++l)
+                if (l < n_out) st16(out[l], pos, acc[l]);
+        } else {
+#pragma unroll
+            for (int l = 0; l < LT; ++l)
+                if (l < n_out) scatter16(out[l], pos, cnt, acc[l]);
+        }
     }
 }
 
