@@ -53,6 +53,8 @@ def parse(argv=None):
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
     ap.add_argument("--engine", default="perm", choices=["perm", "lds"])
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
+    ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
+    ap.add_argument("--e2e-chunk", type=int, default=4096, help="stripes per pipelined chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU work budget (thread-seconds)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -269,14 +271,15 @@ def run_e2e(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
     k, m, n, B, _ = WORKLOADS["rs32_4k"]
     mat = ec.coding_matrix(k, m)
-    chunk = 4096  # stripes per chunk: 16 MiB per shard
+    chunk = args.e2e_chunk  # stripes per chunk (4096: 16 MiB per shard)
+    ns = args.e2e_streams
     nch = B // chunk
     clen = chunk * n
     pin = dict(dtype=torch.uint8, pin_memory=True)
     data_h = [torch.randint(0, 256, (B * n,), dtype=torch.uint8).pin_memory() for _ in range(k)]
     par_h = [torch.empty(B * n, **pin) for _ in range(m)]
     out_h = torch.empty(B * n, **pin)
-    streams = [torch.cuda.Stream() for _ in range(3)]
+    streams = [torch.cuda.Stream() for _ in range(ns)]
     slots = [{"d": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(k)],
               "p": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(m)],
               "o": torch.empty(clen, dtype=torch.uint8, device="cuda")} for _ in streams]
@@ -285,7 +288,7 @@ def run_e2e(args):
 
     def step():
         for c in range(nch):
-            st, sl = streams[c % 3], slots[c % 3]
+            st, sl = streams[c % ns], slots[c % ns]
             lo, hi = c * clen, (c + 1) * clen
             with torch.cuda.stream(st):
                 for j in range(k):
@@ -331,7 +334,7 @@ def run_e2e(args):
             "ms_per_step": round(el * 1e3 / steps, 3), "verified": bool(ok),
             "h2d_bytes_per_stripe": (2 * k) * n, "d2h_bytes_per_stripe": (m + 1) * n,
             "pcie_h2d_GBps_raw": round(h2d, 1), "pcie_d2h_GBps_raw": round(d2h, 1),
-            "config": {"chunk_stripes": chunk, "streams": 3, "stripes": B},
+            "config": {"chunk_stripes": chunk, "streams": ns, "stripes": B},
         }), flush=True)
     plan.destroy()
 
