@@ -719,6 +719,8 @@ CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *conn
     return remaining ? 0u : mask;
 }
 
+#include "cec_drain.inc"
+
 // ============================================================== events / streams
 CEC_API int cec_event_create(void **ev) {
     if (!ev) return fail(CEC_EINVAL, "NULL");

@@ -58,6 +58,17 @@ class Extent(ctypes.Structure):
     ]
 
 
+class HostUpdate(ctypes.Structure):
+    """cec_host_update: one pending rep_queue_item (diff in host memory)."""
+
+    _fields_ = [
+        ("buf", ctypes.c_void_p),
+        ("addr", ctypes.c_uint64),
+        ("len", ctypes.c_uint32),
+        ("src_lid", ctypes.c_uint32),
+    ]
+
+
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _u32 = ctypes.c_uint32
@@ -85,6 +96,10 @@ _SIGS = {
     "cec_solve": ([_i, _i, _ip, _u32, _pp, _pp, _vp, _vp], _i),
     "cec_decode": ([_i, _i, _ip, ctypes.POINTER(_u32), _i, _pp, _pp, _vp, _vp], _i),
     "cec_recovery_mask": ([_i, _i, _i, _ip], _u32),
+    "cec_drainer_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, ctypes.c_size_t], _i),
+    "cec_drainer_destroy": ([_vp], _i),
+    "cec_drainer_apply": ([_vp, ctypes.POINTER(HostUpdate), _i, _vp, _vp], _i),
+    "cec_drainer_last_launches": ([_vp], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
     "cec_event_destroy": ([_vp], _i),
     "cec_event_record": ([_vp, _vp], _i),
@@ -295,6 +310,50 @@ def decode(k, m, matrix, masks: Sequence[int], arenas, out, plan: Plan, stream=N
 
 def recovery_mask(k: int, m: int, leader_lid: int, connected: Sequence[int]) -> int:
     return lib().cec_recovery_mask(k, m, leader_lid, _int_array(connected))
+
+
+def host_updates(updates) -> ctypes.Array:
+    """[(host buffer (numpy / bytearray / pointer), addr, src_lid[, len])] -> cec_host_update[]."""
+    arr = (HostUpdate * len(updates))()
+    for i, u in enumerate(updates):
+        buf, addr, src = u[0], u[1], u[2]
+        n = u[3] if len(u) > 3 else (buf.nbytes if hasattr(buf, "nbytes") else len(buf))
+        arr[i] = HostUpdate(_host_or_dev(buf), addr, n, src)
+    return arr
+
+
+class Drainer:
+    """cec_drainer: batched deferred-commit drain of a parity process (§8f rank 1)."""
+
+    def __init__(self, k: int, m: int, matrix, lid_self: int, staging_bytes: int = 64 << 20):
+        self._h = ctypes.c_void_p()
+        _check(lib().cec_drainer_create(ctypes.byref(self._h), k, m, _int_array(matrix), lid_self,
+                                        staging_bytes))
+
+    def apply(self, updates, parity, stream=None) -> int:
+        """updates: a host_updates() array, or [(host buffer, addr, src_lid[, len])]
+        (the caller keeps the buffers alive).  Returns the launches used."""
+        arr = updates if isinstance(updates, ctypes.Array) else host_updates(updates)
+        _check(lib().cec_drainer_apply(self._h, arr, len(arr), _ptr(parity), _stream(stream)))
+        return lib().cec_drainer_last_launches(self._h)
+
+    def destroy(self) -> None:
+        if self._h:
+            _check(lib().cec_drainer_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.cec_drainer_destroy(self._h)
+        except Exception:
+            pass
 
 
 class Event:

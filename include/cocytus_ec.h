@@ -149,6 +149,34 @@ int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, int n_mas
  * k+m ints.  Returns 0 if fewer than k lids are available. */
 uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected);
 
+/* ---- server-side batching: the parity's deferred-commit drain ----
+ * Replaces the drain loops `while (done_xid < stable_xid) process_rep_command(...)`
+ * (memcached.c:4231, 4322, 4350, 8068) with one call per batch of pending diffs. */
+typedef struct cec_host_update {   /* one pending rep_queue_item (rep_queue.h:28-39) */
+    const void *buf;               /* e->vbuf: the shipped diff, host memory (any kind) */
+    uint64_t addr;                 /* e->addr: arena offset (replayed ecalloc address) */
+    uint32_t len;                  /* it->nbytes */
+    uint32_t src_lid;              /* data shard lid the diff came from (0..k-1) */
+} cec_host_update;
+
+typedef struct cec_drainer cec_drainer;
+
+/* A drainer for parity lid_self owns pinned + device staging of staging_bytes (diffs
+ * larger than that are applied in several rounds) and a reusable tile list. */
+int cec_drainer_create(cec_drainer **out, int k, int m, const int *matrix, int lid_self,
+                       size_t staging_bytes);
+int cec_drainer_destroy(cec_drainer *d);
+
+/* parity[addr..] ^= MATRIX(lid_self, src_lid) * buf for every update, as the sequential
+ * loop of memcached.c:7762-7767 would leave it (XOR accumulation commutes; updates
+ * whose ranges overlap are put in separate launches, never raced).  Synchronous: on
+ * return every update is applied and the host buffers may be reused / acked. */
+int cec_drainer_apply(cec_drainer *d, const cec_host_update *updates, int n,
+                      uint8_t *parity, void *stream);
+
+/* Launches the last cec_drainer_apply needed (>= 1 when n > 0: overlap waves x rounds). */
+int cec_drainer_last_launches(const cec_drainer *d);
+
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
 int cec_event_create(void **ev);
 int cec_event_destroy(void *ev);

@@ -159,3 +159,14 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
     pthread_barrier_destroy(&bar);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64_t *addrs,
+                       const uint32_t *lens, const int *coefs, int n, uint8_t *parity)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < n; ++i)
+        ref_region_multiply_simd(stage + soffs[i], coefs[i], (long)lens[i], parity + addrs[i]);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -121,6 +121,13 @@ int ref_simd_available(void);
 double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
                                int reps, int do_decode);
 
+/* The parity's drain loop as the reference runs it (one thread, memcached.c:4350 ->
+ * process_rep_command -> galois_w08_region_multiply(diff, MATRIX(self, lid), n,
+ * parity + addr, 1) per pending diff): diffs packed at offsets soffs[i].  Returns
+ * elapsed seconds (CLOCK_MONOTONIC). */
+double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64_t *addrs,
+                       const uint32_t *lens, const int *coefs, int n, uint8_t *parity);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,8 @@ _SIGS = {
     "ref_region_multiply_simd": ([ctypes.c_void_p, _i, _l, ctypes.c_void_p], None),
     "ref_simd_available": ([], _i),
     "ref_bench_encode_decode": ([_i, _i, _l, _l, _i, _i, _i], ctypes.c_double),
+    "ref_bench_apply": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                         ctypes.c_void_p, _i, ctypes.c_void_p], ctypes.c_double),
 }
 
 _lib = None
@@ -191,6 +193,16 @@ def simd_available() -> bool:
 
 def bench_encode_decode(k, m, n, nstripes, threads, reps=1, do_decode=True) -> float:
     return lib().ref_bench_encode_decode(k, m, n, nstripes, threads, reps, int(do_decode))
+
+
+def bench_apply(stage: np.ndarray, soffs, addrs, lens, coefs, parity: np.ndarray) -> float:
+    """The reference's single-threaded drain loop over packed diffs; seconds."""
+    so = np.ascontiguousarray(soffs, np.uint64)
+    ad = np.ascontiguousarray(addrs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint32)
+    cf = np.ascontiguousarray(coefs, np.int32)
+    return lib().ref_bench_apply(_p(stage), so.ctypes.data, ad.ctypes.data, ln.ctypes.data,
+                                 cf.ctypes.data, len(ln), _p(parity))
 
 
 def splitmix_bytes(seed: int, n: int) -> np.ndarray:

@@ -400,6 +400,48 @@ def test_cfg4_rs42_64k_roundtrip(gpu, oracle):
         assert np.array_equal(to_host(parity[p][s * n:(s + 1) * n]), ps[p])
 
 
+# ------------------------------------------------------------------ batched drain (§8f 1)
+@pytest.mark.parametrize("staging", [64 << 20, 64 << 10])
+def test_drainer_matches_sequential_loop(gpu, oracle, engine, staging):
+    """cec_drainer_apply == the reference's drain loop (process_rep_command one diff at
+    a time, memcached.c:7762-7767), including overlapping and ragged updates."""
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(staging & 0xFFFF)
+    arena = 1 << 20
+    parity = rng.integers(0, 256, arena, dtype=np.uint8)
+    dev = to_dev(torch, parity)
+    ups = []
+    for i in range(400):
+        n = int(rng.integers(1, 9000)) if i % 5 else 4098
+        addr = int(rng.integers(0, (arena - n) // 16)) * 16 + (3 if i % 37 == 0 else 0)
+        ups.append((rng.integers(0, 256, n, dtype=np.uint8), addr, int(rng.integers(0, k))))
+    lid_self = k + 1
+    with ec.Drainer(k, m, mat, lid_self, staging_bytes=staging) as d:
+        launches = d.apply(ups, dev)
+        launches2 = d.apply([], dev)
+    assert launches >= 2 and launches2 == 0  # overlaps force several waves
+    for buf, addr, j in ups:
+        v = parity[addr:addr + buf.size].copy()
+        oracle.parity_apply(mat, k, lid_self, j, buf, v)
+        parity[addr:addr + buf.size] = v
+    assert np.array_equal(to_host(dev), parity)
+
+
+def test_drainer_rejects_bad_updates(gpu):
+    torch, ec = gpu
+    mat = ec.coding_matrix(3, 2)
+    dev = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with ec.Drainer(3, 2, mat, 3, staging_bytes=8192) as d:
+        with pytest.raises(ec.CecError):
+            d.apply([(np.zeros(10000, np.uint8), 0, 0)], dev)  # larger than staging
+        with pytest.raises(ec.CecError):
+            d.apply([(np.zeros(16, np.uint8), 0, 3)], dev)  # src lid is a parity
+    with pytest.raises(ec.CecError):
+        ec.Drainer(3, 2, mat, 1)  # a data lid cannot drain
+
+
 # ------------------------------------------------------------------ the drop-in symbols
 def test_dropin_host_buffers(gpu, oracle):
     """galois_w08_region_multiply on pageable host memory at arbitrary alignment."""
