@@ -720,6 +720,7 @@ CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *conn
 }
 
 #include "cec_drain.inc"
+#include "cec_recovery.inc"
 
 // ============================================================== events / streams
 CEC_API int cec_event_create(void **ev) {

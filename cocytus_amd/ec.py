@@ -100,6 +100,14 @@ _SIGS = {
     "cec_drainer_destroy": ([_vp], _i),
     "cec_drainer_apply": ([_vp, ctypes.POINTER(HostUpdate), _i, _vp, _vp], _i),
     "cec_drainer_last_launches": ([_vp], _i),
+    "cec_recovery_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, _u32, _i, _i, _vp, _vp], _i),
+    "cec_recovery_destroy": ([_vp], _i),
+    "cec_recovery_add_peer": ([_vp, _i, _vp, _vp], _i),
+    "cec_recovery_fold_update": ([_vp, _i, ctypes.c_uint64, _vp, _u32, _vp], _i),
+    "cec_recovery_complete": ([_vp], _i),
+    "cec_recovery_residual": ([_vp], _vp),
+    "cec_recovery_bytes": ([_vp], ctypes.c_uint64),
+    "cec_recovery_solve": ([_vp, _pp, _pp, _vp], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
     "cec_event_destroy": ([_vp], _i),
     "cec_event_record": ([_vp, _vp], _i),
@@ -352,6 +360,65 @@ class Drainer:
         try:
             if self._h and _lib is not None:
                 _lib.cec_drainer_destroy(self._h)
+        except Exception:
+            pass
+
+
+class Recovery:
+    """cec_recovery: one online-recovery request on a participating parity (§8f rank 2).
+
+    Buffers may be host (numpy / bytearray) or device (tensor / int pointer)."""
+
+    def __init__(self, k, m, matrix, lid_self, mask, unit_begin, unit_end, parity_arena, stream=None):
+        self.k, self.m = k, m
+        self._h = ctypes.c_void_p()
+        _check(lib().cec_recovery_create(ctypes.byref(self._h), k, m, _int_array(matrix), lid_self, mask,
+                                         unit_begin, unit_end, _ptr(parity_arena), _stream(stream)))
+
+    def add_peer(self, peer_lid: int, units, stream=None) -> None:
+        _check(lib().cec_recovery_add_peer(self._h, peer_lid, _host_or_dev(units), _stream(stream)))
+
+    def fold_update(self, peer_lid: int, addr: int, diff, stream=None) -> int:
+        n = diff.nbytes if hasattr(diff, "nbytes") else len(diff)
+        rc = lib().cec_recovery_fold_update(self._h, peer_lid, addr, _host_or_dev(diff), n, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    @property
+    def complete(self) -> bool:
+        return bool(lib().cec_recovery_complete(self._h))
+
+    @property
+    def residual(self) -> int:
+        return int(lib().cec_recovery_residual(self._h) or 0)
+
+    @property
+    def nbytes(self) -> int:
+        return int(lib().cec_recovery_bytes(self._h))
+
+    def solve(self, peer_residuals: dict, out: dict, stream=None) -> None:
+        """peer_residuals / out: {lid: buffer} (host or device)."""
+        pr = (ctypes.c_void_p * (self.k + self.m))(*[_host_or_dev(peer_residuals.get(i)) or None
+                                                     for i in range(self.k + self.m)])
+        oo = (ctypes.c_void_p * self.k)(*[_host_or_dev(out.get(j)) or None for j in range(self.k)])
+        _check(lib().cec_recovery_solve(self._h, pr, oo, _stream(stream)))
+
+    def destroy(self) -> None:
+        if self._h:
+            _check(lib().cec_recovery_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.cec_recovery_destroy(self._h)
         except Exception:
             pass
 

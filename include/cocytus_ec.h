@@ -177,6 +177,48 @@ int cec_drainer_apply(cec_drainer *d, const cec_host_update *updates, int n,
 /* Launches the last cec_drainer_apply needed (>= 1 when n > 0: overlap waves x rounds). */
 int cec_drainer_last_launches(const cec_drainer *d);
 
+/* ---- online recovery over 4 KiB unit ranges ----
+ * One recovery request on a participating parity (recovery_queue_item,
+ * recovery.h:57-69): units [unit_begin, unit_end] (UNITSIZE = 4 KiB, const.h:26) of
+ * the arenas, participants `mask` (start_recovery, memcached.c:8136-8151).  The
+ * residual lives in HBM.  Peer data, diffs and the other parities' residuals may be
+ * host memory (pageable or pinned: staged through a pipelined pinned uploader) or
+ * device memory (used in place).  All calls are synchronous. */
+typedef struct cec_recovery cec_recovery;
+
+int cec_recovery_create(cec_recovery **out, int k, int m, const int *matrix, int lid_self,
+                        uint32_t mask, int unit_begin, int unit_end,
+                        const uint8_t *parity_arena /* device: this parity's arena */,
+                        void *stream);
+int cec_recovery_destroy(cec_recovery *r);
+
+/* recovery_recover_units (recovery.c:61-96): data peer peer_lid (in mask, not yet
+ * applied) sent its raw bytes of the whole range (nbuf bytes).  The first peer also
+ * copies the parity units in (first touch, recovery.c:79-82), fused into one pass. */
+int cec_recovery_add_peer(cec_recovery *r, int peer_lid, const void *units, void *stream);
+
+/* recovery_try_update_unit (recovery.c:99-131): a diff of len bytes at arena address
+ * addr from data peer peer_lid reached this parity during recovery.  It is folded into
+ * the residual where the range is touched and the peer has not contributed yet.
+ * Returns the number of units folded (>= 0) or a negative cec_status. */
+int cec_recovery_fold_update(cec_recovery *r, int peer_lid, uint64_t addr, const void *diff,
+                             uint32_t len, void *stream);
+
+/* check_recovery_1st_completeness (memcached.c:2522-2545): 1 when every data lid of
+ * the mask has contributed, else 0. */
+int cec_recovery_complete(const cec_recovery *r);
+
+/* The residual (device memory, cec_recovery_bytes(r) bytes). */
+const uint8_t *cec_recovery_residual(const cec_recovery *r);
+uint64_t cec_recovery_bytes(const cec_recovery *r);
+
+/* Leader (complete_recovery_bottom_half, memcached.c:7842-7922): C[j] = residual of
+ * the j-th parity in the mask (this session's own for lid_self; peer_residuals[lid]
+ * for the others, host or device); out[lost lid] (host or device, nbuf bytes each) =
+ * sum_j inv[i][j] * C[j] for the n lost data lids. */
+int cec_recovery_solve(cec_recovery *leader, const void *const *peer_residuals,
+                       void *const *out, void *stream);
+
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
 int cec_event_create(void **ev);
 int cec_event_destroy(void *ev);

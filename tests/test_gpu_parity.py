@@ -442,6 +442,89 @@ def test_drainer_rejects_bad_updates(gpu):
         ec.Drainer(3, 2, mat, 1)  # a data lid cannot drain
 
 
+# ------------------------------------------------------------------ recovery sessions (§8f 2)
+@pytest.mark.parametrize("host_inputs", [True, False])
+def test_recovery_session_single_loss_with_updates(gpu, oracle, host_inputs):
+    """D0 lost, leader P0 (mask {D1, D2, P0}); writes from D1/D2 land while the
+    recovery is in flight (recovery.c:99-131); the rebuilt D0 equals the live data."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(8 + host_inputs)
+    nunits, ub, ue = 96, 10, 73
+    data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    p0 = to_dev(torch, parity[0])
+    mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])
+    lo, hi = ub * U, (ue + 1) * U
+
+    def land_update(rec, s):  # a SET on data peer s: diff to the parity (+ fold)
+        n = int(rng.integers(1, 9000))
+        addr = int(rng.integers(lo - 5000, hi - n + 5000)) // 16 * 16
+        addr = max(0, min(addr, nunits * U - n))
+        new = rng.integers(0, 256, n, dtype=np.uint8)
+        diff = oracle.set_diff(data[s][addr:addr + n].copy(), new)
+        data[s][addr:addr + n] = new
+        rec.fold_update(s, addr, diff if host_inputs else to_dev(torch, diff))
+        ec.region_multiply(to_dev(torch, diff), mat[3 * k + s], n, p0.data_ptr() + addr, 1)  # memcached.c:7764
+        torch.cuda.synchronize()
+
+    with ec.Recovery(k, m, mat, 3, mask, ub, ue, p0) as rec:
+        assert rec.nbytes == hi - lo and not rec.complete
+        land_update(rec, 1)                      # before any peer: picked up at first touch
+        units1 = data[1][lo:hi].copy()
+        rec.add_peer(1, units1 if host_inputs else to_dev(torch, units1))
+        land_update(rec, 1)                      # peer 1 already sent: no fold
+        land_update(rec, 2)                      # peer 2 not yet: folded
+        land_update(rec, 2)
+        assert not rec.complete
+        units2 = data[2][lo:hi].copy()
+        rec.add_peer(2, units2 if host_inputs else to_dev(torch, units2))
+        assert rec.complete
+        with pytest.raises(ec.CecError):
+            rec.add_peer(2, units2)              # recovery.c:75 asserts a peer applies once
+        if host_inputs:
+            out = np.zeros(hi - lo, np.uint8)
+            rec.solve({}, {0: out})
+        else:
+            dout = torch.zeros(hi - lo, dtype=torch.uint8, device="cuda")
+            rec.solve({}, {0: dout})
+            out = to_host(dout)
+    assert np.array_equal(out, data[0][lo:hi])
+
+
+def test_recovery_sessions_double_loss_leader_solve(gpu, oracle):
+    """D0 and D1 lost; P0 and P1 each build a residual from D2; the leader P0 solves with
+    P1's residual shipped as host bytes (recover_units_gather) -> both shards rebuilt;
+    residuals equal the reference chain (recovery_recover_units)."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    n = 40 * U
+    data = [oracle.splitmix_bytes(0xC0C70005 + j, n) for j in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    pdev = [to_dev(torch, p) for p in parity]
+    mask = 0b11100
+    with ec.Recovery(k, m, mat, 3, mask, 0, 39, pdev[0]) as r0, \
+         ec.Recovery(k, m, mat, 4, mask, 0, 39, pdev[1]) as r1:
+        r0.add_peer(2, data[2])
+        r1.add_peer(2, data[2])
+        tmp = torch.empty(n, dtype=torch.uint8, device="cuda")
+        res = {}
+        for p, rec in ((3, r0), (4, r1)):
+            ec.region_multiply(rec.residual, 1, n, tmp, 0)  # copy the device residual out
+            torch.cuda.synchronize()
+            res[p] = to_host(tmp)
+            exp = np.empty(n, np.uint8)
+            touched = [0]
+            oracle.recover_units(mat, k, p, 2, parity[p - k], data[2], exp, touched)
+            assert np.array_equal(res[p], exp), p
+        res1 = res[4]
+        out0, out1 = np.zeros(n, np.uint8), np.zeros(n, np.uint8)
+        r0.solve({4: res1}, {0: out0, 1: out1})
+    assert np.array_equal(out0, data[0]) and np.array_equal(out1, data[1])
+
+
 # ------------------------------------------------------------------ the drop-in symbols
 def test_dropin_host_buffers(gpu, oracle):
     """galois_w08_region_multiply on pageable host memory at arbitrary alignment."""
