@@ -55,6 +55,7 @@ def parse(argv=None):
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
     ap.add_argument("--drain", action="store_true", help="batched parity drain from host diffs")
+    ap.add_argument("--recovery", action="store_true", help="online recovery session, host survivors")
     ap.add_argument("--e2e-chunk", type=int, default=4096, help="stripes per pipelined chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU work budget (thread-seconds)")
@@ -393,6 +394,59 @@ def run_drain(args):
         }), flush=True)
 
 
+def run_recovery(args):
+    """the leader parity P0 recovers lost D0 over a 256 MiB range
+    (65,536 units): survivors D1, D2 arrive as host bytes (recover_units_reply), the
+    parity arena is in HBM, the rebuilt shard goes back to host memory.  GPU: one
+    cec_recovery (add_peer x 2 + solve).  CPU: the reference's chain on one thread
+    (per-unit residual, then the bottom half), restated GF-Complete kernel."""
+    import numpy as np
+
+    torch, dist, ec, world, rank = setup(args.dist_backend)
+    from oracle import pyoracle
+
+    k, m, U, nunits = 3, 2, 4096, 65536
+    n = U * nunits
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70005)
+    data = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, parity, n)
+    torch.cuda.synchronize()
+    host = [d.cpu().numpy() for d in data]
+    mask = ec.recovery_mask(k, m, k, [0, 1, 1, 1, 1])  # D0 lost, leader P0
+    out = np.zeros(n, np.uint8)
+    with ec.Recovery(k, m, mat, k, mask, 0, nunits - 1, parity[0]) as warm:
+        warm.add_peer(1, host[1])
+        warm.add_peer(2, host[2])
+        warm.solve({}, {0: out})
+    steps = max(1, min(args.steps, 10))
+    t = 0.0
+    for _ in range(steps):
+        with ec.Recovery(k, m, mat, k, mask, 0, nunits - 1, parity[0]) as rec:
+            t0 = time.perf_counter()
+            rec.add_peer(1, host[1])
+            rec.add_peer(2, host[2])
+            rec.solve({}, {0: out})
+            t += time.perf_counter() - t0
+    ok = np.array_equal(out, host[0])
+    p0 = parity[0].cpu().numpy()
+    t_cpu, cpu_out = pyoracle.bench_recover(p0, [host[1], host[2]], [mat[k * k + 1], mat[k * k + 2]],
+                                            pyoracle.gf_div(1, mat[k * k + 0]))
+    ok &= np.array_equal(cpu_out, host[0])
+    gib = n / 2**30
+    if rank == 0:
+        print(json.dumps({
+            "metric": "GiB/s online recovery of one lost data shard, 65,536 x 4 KiB units, host survivors -> host rebuilt",
+            "value": round(gib * steps / t, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+            "ms_per_step": round(t * 1e3 / steps, 3), "verified": bool(ok),
+            "includes": "H2D of 2 survivor ranges (pipelined pinned staging) + residual kernels + solve + D2H",
+            "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+                             "sample": "the reference's recovery chain for the same range on one thread "
+                                       "(recovery.c:72-94 per unit, memcached.c:7913-7922), restated GF-Complete AVX2"},
+        }), flush=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
@@ -401,6 +455,8 @@ def main():
         run_e2e(args)
     elif args.drain:
         run_drain(args)
+    elif args.recovery:
+        run_recovery(args)
     else:
         run_device(args)
     import torch.distributed as dist

@@ -160,6 +160,24 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
+double ref_bench_recover(const uint8_t *parity, const uint8_t *const *peers, const int *coefs,
+                         int npeers, int inv, long nbuf, uint8_t *residual, uint8_t *out)
+{
+    const long unit = 4096;
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int p = 0; p < npeers; ++p)
+        for (long u = 0; u < nbuf; u += unit) {
+            const long len = nbuf - u < unit ? nbuf - u : unit;
+            if (p == 0) memcpy(residual + u, parity + u, (size_t)len);
+            ref_region_multiply_simd(peers[p] + u, coefs[p], len, residual + u);
+        }
+    memset(out, 0, (size_t)nbuf);
+    ref_region_multiply_simd(residual, inv, nbuf, out);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64_t *addrs,
                        const uint32_t *lens, const int *coefs, int n, uint8_t *parity)
 {

@@ -128,6 +128,13 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
 double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64_t *addrs,
                        const uint32_t *lens, const int *coefs, int n, uint8_t *parity);
 
+/* One parity's online recovery of a single lost data shard over nbuf bytes as the
+ * reference runs it (one thread): per peer message, per 4 KiB unit, first touch copies
+ * the parity unit then region-multiplies the peer unit in (recovery.c:72-94); then the
+ * leader's bottom half into a zeroed buffer (memcached.c:7913-7922).  Seconds. */
+double ref_bench_recover(const uint8_t *parity, const uint8_t *const *peers, const int *coefs,
+                         int npeers, int inv, long nbuf, uint8_t *residual, uint8_t *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -45,6 +45,8 @@ _SIGS = {
     "ref_bench_encode_decode": ([_i, _i, _l, _l, _i, _i, _i], ctypes.c_double),
     "ref_bench_apply": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.c_void_p, _i, ctypes.c_void_p], ctypes.c_double),
+    "ref_bench_recover": ([ctypes.c_void_p, _vpp, ctypes.c_void_p, _i, _i, _l, ctypes.c_void_p,
+                           ctypes.c_void_p], ctypes.c_double),
 }
 
 _lib = None
@@ -203,6 +205,17 @@ def bench_apply(stage: np.ndarray, soffs, addrs, lens, coefs, parity: np.ndarray
     cf = np.ascontiguousarray(coefs, np.int32)
     return lib().ref_bench_apply(_p(stage), so.ctypes.data, ad.ctypes.data, ln.ctypes.data,
                                  cf.ctypes.data, len(ln), _p(parity))
+
+
+def bench_recover(parity: np.ndarray, peers: list, coefs, inv: int) -> tuple[float, np.ndarray]:
+    """The reference's one-parity recovery chain (residual + leader solve); (s, out)."""
+    n = parity.size
+    res = np.empty(n, np.uint8)
+    out = np.empty(n, np.uint8)
+    cf = np.ascontiguousarray(coefs, np.int32)
+    t = lib().ref_bench_recover(_p(parity), _arr(peers), cf.ctypes.data, len(peers), inv, n,
+                                _p(res), _p(out))
+    return t, out
 
 
 def splitmix_bytes(seed: int, n: int) -> np.ndarray:
