@@ -171,7 +171,8 @@ def run_device(args):
     masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
              for p in range(m) for j in range(k)]
     enc_plan = ec.Plan([(o, 0, ln, 0) for o, ln in stripes])
-    dec_plan = ec.Plan([(o, 0, ln, s % len(masks)) for s, (o, ln) in enumerate(stripes)])
+    dec_ext = [(o, 0, ln, s % len(masks)) for s, (o, ln) in enumerate(stripes)]
+    dec_plan = ec.Plan(dec_ext)
     stream = torch.cuda.current_stream()
     bytes_total = sum(ln for _, ln in stripes)
 

@@ -1,0 +1,113 @@
+// tools/hbm_mix.hip -- HBM ceiling per read:write mix on this MI355X (not product).
+// Each kernel streams R read arenas and W write arenas of `len` bytes with the access
+// shape of combine_kernel (one 4 KiB tile per 256-lane workgroup, 16 B per lane, nt
+// loads/stores), XOR-combining reads into every write; grid = tiles.  The GB/s of
+// each mix is the practical roofline for the op with that mix:
+//   encode RS(3,2) 3:2, decode single 3:1, RS(4,2) encode 4:2, drain 2:1 (RMW).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbm_mix.hip -o tools/hbm_mix.bin
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e = (x);                                                \
+        if (e != hipSuccess) {                                             \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));         \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define GL __attribute__((address_space(1)))
+
+struct Ptrs {
+    const uint8_t *r[6];
+    uint8_t *w[4];
+};
+
+template <int R, int W>
+__global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
+    const uint64_t off = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < R; ++i)
+        acc ^= __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)p.r[i] + off));
+    if constexpr (W == 0) {
+        if ((acc.x ^ acc.y ^ acc.z ^ acc.w) == 0x12345678u) sink[0] = 1;  // keep the loads
+    } else {
+#pragma unroll
+        for (int j = 0; j < W; ++j) {
+            u32x4 v = acc;
+            v.x ^= j;
+            __builtin_nontemporal_store(v, (GL u32x4 *)((uintptr_t)p.w[j] + off));
+        }
+    }
+}
+
+int main() {
+    const uint64_t len = 256ull << 20;  // per arena
+    Ptrs p;
+    std::vector<uint8_t *> bufs;
+    for (int i = 0; i < 10; ++i) {
+        uint8_t *b;
+        CK(hipMalloc(&b, len));
+        CK(hipMemset(b, i * 7 + 1, len));
+        bufs.push_back(b);
+    }
+    for (int i = 0; i < 6; ++i) p.r[i] = bufs[i];
+    for (int j = 0; j < 4; ++j) p.w[j] = bufs[6 + j];
+    uint32_t *sink;
+    CK(hipMalloc(&sink, 4));
+    struct V {
+        const char *name;
+        int r, w;
+    };
+    std::vector<V> vs = {{"read 1", 1, 0}, {"read 3", 3, 0}, {"write 1 (from read 0)", 0, 1},
+                         {"1:1 copy", 1, 1}, {"2:1 (RMW-like)", 2, 1}, {"3:1 decode RS(3,2)", 3, 1},
+                         {"3:2 encode RS(3,2)", 3, 2}, {"4:1 decode RS(4,2)", 4, 1},
+                         {"4:2 encode RS(4,2)", 4, 2}, {"6:4 RS(6,4)-like", 6, 4}};
+    const uint32_t grid = len / 4096;
+    auto launch = [&](const V &v) {
+        switch (v.r * 10 + v.w) {
+        case 10: hipLaunchKernelGGL((k_mix<1, 0>), grid, 256, 0, 0, p, sink); break;
+        case 30: hipLaunchKernelGGL((k_mix<3, 0>), grid, 256, 0, 0, p, sink); break;
+        case 1: hipLaunchKernelGGL((k_mix<0, 1>), grid, 256, 0, 0, p, sink); break;
+        case 11: hipLaunchKernelGGL((k_mix<1, 1>), grid, 256, 0, 0, p, sink); break;
+        case 21: hipLaunchKernelGGL((k_mix<2, 1>), grid, 256, 0, 0, p, sink); break;
+        case 31: hipLaunchKernelGGL((k_mix<3, 1>), grid, 256, 0, 0, p, sink); break;
+        case 32: hipLaunchKernelGGL((k_mix<3, 2>), grid, 256, 0, 0, p, sink); break;
+        case 41: hipLaunchKernelGGL((k_mix<4, 1>), grid, 256, 0, 0, p, sink); break;
+        case 42: hipLaunchKernelGGL((k_mix<4, 2>), grid, 256, 0, 0, p, sink); break;
+        case 64: hipLaunchKernelGGL((k_mix<6, 4>), grid, 256, 0, 0, p, sink); break;
+        }
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int rounds = 7, iters = 10;
+    std::vector<std::vector<float>> ms(vs.size());
+    for (int r = 0; r < rounds; ++r)
+        for (size_t i = 0; i < vs.size(); ++i) {
+            launch(vs[i]);
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < iters; ++it) launch(vs[i]);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            ms[i].push_back(t / iters);
+        }
+    printf("HBM ceilings by read:write mix, %llu MiB per arena, 4 KiB tile per workgroup, nt\n",
+           (unsigned long long)(len >> 20));
+    for (size_t i = 0; i < vs.size(); ++i) {
+        std::sort(ms[i].begin(), ms[i].end());
+        const double bytes = (double)(vs[i].r + vs[i].w) * len;
+        printf("%-24s median %.4f ms -> %.0f GB/s (best %.0f)\n", vs[i].name, ms[i][rounds / 2],
+               bytes / (ms[i][rounds / 2] * 1e6), bytes / (ms[i][0] * 1e6));
+    }
+    return 0;
+}
