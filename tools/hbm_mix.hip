@@ -48,16 +48,31 @@ __global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
     }
 }
 
-int main() {
+int main(int argc, char **argv) {
     const uint64_t len = 256ull << 20;  // per arena
+    // argv[1] = skew in bytes: arena i starts i * skew past a 2 MiB boundary inside one
+    // allocation (0 = separate hipMalloc per arena, the default layout)
+    const uint64_t skew = argc > 1 ? strtoull(argv[1], nullptr, 0) : 0;
     Ptrs p;
     std::vector<uint8_t *> bufs;
-    for (int i = 0; i < 10; ++i) {
-        uint8_t *b;
-        CK(hipMalloc(&b, len));
-        CK(hipMemset(b, i * 7 + 1, len));
-        bufs.push_back(b);
+    if (skew == 0) {
+        for (int i = 0; i < 10; ++i) {
+            uint8_t *b;
+            CK(hipMalloc(&b, len));
+            CK(hipMemset(b, i * 7 + 1, len));
+            bufs.push_back(b);
+        }
+    } else {
+        const uint64_t stride = len + (2ull << 20);
+        uint8_t *big;
+        CK(hipMalloc(&big, 10 * stride + 10 * skew));
+        for (int i = 0; i < 10; ++i) {
+            uint8_t *b = big + i * stride + i * skew;
+            CK(hipMemset(b, i * 7 + 1, len));
+            bufs.push_back(b);
+        }
     }
+    printf("arena skew: %llu bytes\n", (unsigned long long)skew);
     for (int i = 0; i < 6; ++i) p.r[i] = bufs[i];
     for (int j = 0; j < 4; ++j) p.w[j] = bufs[6 + j];
     uint32_t *sink;
