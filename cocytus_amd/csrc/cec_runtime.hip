@@ -726,7 +726,9 @@ CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *conn
 CEC_API int cec_event_create(void **ev) {
     if (!ev) return fail(CEC_EINVAL, "NULL");
     hipEvent_t e;
-    HIP_TRY(hipEventCreate(&e));
+    // Timing events only: no system-scope fence at record (the default fence writes the
+    // L2 back between launches, which lengthens the measured interval).
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
     *ev = e;
     return CEC_OK;
 }

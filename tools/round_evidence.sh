@@ -1,0 +1,23 @@
+#!/bin/bash
+# tools/round_evidence.sh ROUND -- every measurement DESIGN.md quotes, on one box, one call
+# (run ON the GPU box through gpurun).  Results land in gpurun_out/evidence_ROUND/;
+# copy what is quoted into profiles/ (tools/collect_evidence.py does it here).
+set -euo pipefail
+ROUND=${1:-r01}
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+OUT=$R/gpurun_out/evidence_$ROUND
+mkdir -p "$OUT"
+cd "$R"
+B="timeout -k 10 300 python bench.py"
+$B                                     > "$OUT/bench_default.jsonl" 2> "$OUT/bench_default.err"
+$B --no-cpu-baseline --engine lds      > "$OUT/bench_lds.jsonl"     2> "$OUT/bench_lds.err"
+$B --no-cpu-baseline --workload rs32_mixed > "$OUT/bench_mixed.jsonl" 2> "$OUT/bench_mixed.err"
+$B --no-cpu-baseline --workload rs42_64k   > "$OUT/bench_rs42.jsonl"  2> "$OUT/bench_rs42.err"
+$B --no-cpu-baseline --workload rs32_1m    > "$OUT/bench_1m.jsonl"    2> "$OUT/bench_1m.err"
+$B --e2e                               > "$OUT/bench_e2e.jsonl"     2> "$OUT/bench_e2e.err"
+$B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/bench_drain.err"
+$B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"
+timeout -k 10 200 tools/hbm_mix.bin    > "$OUT/hbm_mix.txt" 2>&1
+timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
+bash tools/profile_round.sh "$ROUND"   > "$OUT/profile.log" 2>&1
+echo done > "$OUT/DONE"
