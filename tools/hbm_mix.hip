@@ -48,18 +48,36 @@ __global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
     }
 }
 
+// splitmix64 fill: the ceilings must be measured on random bytes like the bench's
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
 int main(int argc, char **argv) {
     const uint64_t len = 256ull << 20;  // per arena
     // argv[1] = skew in bytes: arena i starts i * skew past a 2 MiB boundary inside one
     // allocation (0 = separate hipMalloc per arena, the default layout)
     const uint64_t skew = argc > 1 ? strtoull(argv[1], nullptr, 0) : 0;
+    // argv[2] == "const": constant bytes (hipMemset) instead of random ones
+    const bool constant = argc > 2 && argv[2][0] == 'c';
+    auto fill = [&](uint8_t *b, int i) {
+        if (constant) CK(hipMemset(b, i * 7 + 1, len));
+        else hipLaunchKernelGGL(k_fill, 4096, 256, 0, 0, (uint64_t *)b, len / 8, 0xC0C70000ull + i);
+        CK(hipDeviceSynchronize());
+    };
+    printf("fill: %s\n", constant ? "constant" : "random");
     Ptrs p;
     std::vector<uint8_t *> bufs;
     if (skew == 0) {
         for (int i = 0; i < 10; ++i) {
             uint8_t *b;
             CK(hipMalloc(&b, len));
-            CK(hipMemset(b, i * 7 + 1, len));
+            fill(b, i);
             bufs.push_back(b);
         }
     } else {
@@ -68,7 +86,7 @@ int main(int argc, char **argv) {
         CK(hipMalloc(&big, 10 * stride + 10 * skew));
         for (int i = 0; i < 10; ++i) {
             uint8_t *b = big + i * stride + i * skew;
-            CK(hipMemset(b, i * 7 + 1, len));
+            fill(b, i);
             bufs.push_back(b);
         }
     }
