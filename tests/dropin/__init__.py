@@ -23,6 +23,19 @@ def build_dropin(out_dir: str) -> str:
     return exe
 
 
+def run_dropin_threads(tmp_path, threads=8, iters=200) -> str:
+    exe = os.path.join(str(tmp_path), "dropin_threads")
+    subprocess.run(
+        ["gcc", "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
+         os.path.join(HERE, "dropin_threads.c"), "-L", LIBDIR, "-lJerasure", "-lpthread",
+         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+        check=True,
+    )
+    r = subprocess.run([exe, str(threads), str(iters)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout
+    return r.stdout
+
+
 def run_dropin_case(oracle, tmp_path, K=3, M=2, seed=0xC0C70001) -> None:
     rng = np.random.default_rng(seed)
     arena = 64 * 4096

@@ -560,3 +560,49 @@ def test_dropin_c_program(gpu, oracle, tmp_path):
     from tests.dropin import run_dropin_case
 
     run_dropin_case(oracle, tmp_path)
+
+
+def test_dropin_reentrant_threads(gpu, tmp_path):
+    """8 pthreads call the drop-in concurrently (all four argument forms, sizes up to
+    300 KB so both the zero-copy and the staged path run, odd alignments); each checks
+    against its own scalar GF(2^8)."""
+    from tests.dropin import run_dropin_threads
+
+    out = run_dropin_threads(tmp_path, threads=8, iters=150)
+    assert "0 mismatches" in out
+
+
+def test_edge_cases(gpu, oracle):
+    """Empty plans and zero-length extents, k+m at the limit, bad masks / patterns."""
+    torch, ec = gpu
+    k, m = 16, 8  # CEC_MAX_K, CEC_MAX_M
+    mat = ec.coding_matrix(k, m)
+    assert mat == oracle.big_vandermonde(k + m, k)
+    n = 3 * 4096 + 5
+    data = [oracle.splitmix_bytes(500 + j, n) for j in range(k)]
+    ddev = [to_dev(torch, d) for d in data]
+    pdev = [to_dev(torch, np.zeros(n, np.uint8)) for _ in range(m)]
+    with ec.Plan([(0, 0, n, 0), (0, 0, 0, 0)]) as plan:  # a zero-length extent
+        ec.encode(k, m, mat, ddev, pdev, plan)
+        torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, data)
+    for p in range(m):
+        assert np.array_equal(to_host(pdev[p]), exp[p])
+    # k = 16 decode of 8 lost data shards (max width: 16 inputs x 8 outputs)
+    mask = sum(1 << x for x in list(range(8, 16)) + list(range(16, 24)))
+    odev = [to_dev(torch, np.zeros(n, np.uint8)) for _ in range(k)]
+    with ec.Plan([(0, 0, n, 0)]) as plan:
+        ec.decode(k, m, mat, [mask], ddev + pdev, odev, plan)
+        torch.cuda.synchronize()
+    for j in range(8):
+        assert np.array_equal(to_host(odev[j]), data[j]), j
+    with ec.Plan([]) as empty:  # empty plan: every op is a no-op
+        assert empty.num_tiles == 0
+        ec.encode(k, m, mat, ddev, pdev, empty)
+    with ec.Plan([(0, 0, 16, 1)]) as plan:
+        with pytest.raises(ec.CecError):  # pattern index beyond the masks given
+            ec.decode(3, 2, ec.coding_matrix(3, 2), [0b01110], ddev[:5], odev[:3], plan)
+        with pytest.raises(ec.CecError):  # mask without k members
+            ec.decode(3, 2, ec.coding_matrix(3, 2), [0b00011, 0b0111], ddev[:5], odev[:3], plan)
+    with pytest.raises(ec.CecError):
+        ec.encode_region(17, 2, [1] * 19 * 17, ddev[:17] + [ddev[0]], pdev[:2], 16)
