@@ -572,6 +572,44 @@ def test_dropin_reentrant_threads(gpu, tmp_path):
     assert "0 mismatches" in out
 
 
+def test_graph_capture_replay(gpu, oracle):
+    """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
+    bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
+    torch, ec = gpu
+    k, m, n, B = 3, 2, 4096, 512
+    mat = ec.coding_matrix(k, m)
+    host = [oracle.splitmix_bytes(0xC0C70002 + j, B * n) for j in range(k)]
+    data = [to_dev(torch, h) for h in host]
+    parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
+             for p in range(m) for j in range(k)]
+    ep = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
+    dp = ec.Plan([(s * n, 0, n, s % 6) for s in range(B)])
+    ec.encode(k, m, mat, data, parity, ep)  # warm the pattern cache (no allocation in capture)
+    ec.decode(k, m, mat, masks, data + parity, out, dp)
+    torch.cuda.synchronize()
+    for t in parity + out:
+        t.zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream()
+        ec.encode(k, m, mat, data, parity, ep, s)
+        ec.decode(k, m, mat, masks, data + parity, out, dp, s)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, host)
+    for p in range(m):
+        assert np.array_equal(to_host(parity[p]), exp[p])
+    for q, mk in enumerate(masks):
+        j = [x for x in range(k) if not (mk >> x) & 1][0]
+        sel = torch.arange(q, B, len(masks), device="cuda")
+        assert torch.equal(out[j].view(B, n)[sel], data[j].view(B, n)[sel])
+    ep.destroy()
+    dp.destroy()
+
+
 def test_edge_cases(gpu, oracle):
     """Empty plans and zero-length extents, k+m at the limit, bad masks / patterns."""
     torch, ec = gpu

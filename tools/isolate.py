@@ -60,3 +60,14 @@ for rnd in range(3):
     print(f"round {rnd}: encode-only {5 * B * n / te / 1e6:.0f} GB/s ({te:.4f} ms)  "
           f"encode_region {5 * B * n / tr / 1e6:.0f}  decode-only {4 * B * n / td / 1e6:.0f} GB/s ({td:.4f} ms)  "
           f"alternating step {ta:.4f} ms (sum of singles {te + td:.4f})", flush=True)
+
+# ---- HIP graph replay of the encode + decode step vs eager launches
+g = torch.cuda.CUDAGraph()
+with torch.cuda.graph(g):
+    s2 = torch.cuda.current_stream()
+    ec.encode(k, m, mat, data, parity, ep, s2)
+    ec.decode(k, m, mat, masks, data + parity, out, dp, s2)
+for rnd in range(3):
+    tg = timed(lambda: g.replay())
+    ta = timed(lambda: (enc(), dec()))
+    print(f"round {rnd}: graph step {tg:.4f} ms  eager step {ta:.4f} ms", flush=True)
