@@ -100,6 +100,7 @@ _SIGS = {
     "cec_drainer_destroy": ([_vp], _i),
     "cec_drainer_apply": ([_vp, ctypes.POINTER(HostUpdate), _i, _vp, _vp], _i),
     "cec_drainer_last_launches": ([_vp], _i),
+    "cec_drainer_staging": ([_vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.POINTER(ctypes.c_uint8)),
     "cec_recovery_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, _u32, _i, _i, _vp, _vp], _i),
     "cec_recovery_destroy": ([_vp], _i),
     "cec_recovery_add_peer": ([_vp, _i, _vp, _vp], _i),
@@ -344,6 +345,16 @@ class Drainer:
         arr = updates if isinstance(updates, ctypes.Array) else host_updates(updates)
         _check(lib().cec_drainer_apply(self._h, arr, len(arr), _ptr(parity), _stream(stream)))
         return lib().cec_drainer_last_launches(self._h)
+
+    def staging(self):
+        """(address, numpy uint8 view) of the drainer's pinned staging area: diffs
+        received straight into it are applied without a pack copy."""
+        import numpy as np
+
+        cap = ctypes.c_size_t()
+        p = lib().cec_drainer_staging(self._h, ctypes.byref(cap))
+        addr = ctypes.cast(p, ctypes.c_void_p).value
+        return addr, np.ctypeslib.as_array((ctypes.c_uint8 * cap.value).from_address(addr))
 
     def destroy(self) -> None:
         if self._h:

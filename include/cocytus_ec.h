@@ -177,6 +177,13 @@ int cec_drainer_apply(cec_drainer *d, const cec_host_update *updates, int n,
 /* Launches the last cec_drainer_apply needed (>= 1 when n > 0: overlap waves x rounds). */
 int cec_drainer_last_launches(const cec_drainer *d);
 
+/* The drainer's pinned staging area (2 x staging_bytes; *capacity receives its size).
+ * A server can receive diffs straight into it (conn_nread of the "rep" payload,
+ * memcached.c:7727-7735, into e->vbuf carved from this area).  When every update of a
+ * cec_drainer_apply call points into it, the call skips the pack copy: one H2D of the
+ * used span, then the fold.  The caller must not write the area during an apply. */
+uint8_t *cec_drainer_staging(cec_drainer *d, size_t *capacity);
+
 /* ---- online recovery over 4 KiB unit ranges ----
  * One recovery request on a participating parity (recovery_queue_item,
  * recovery.h:57-69): units [unit_begin, unit_end] (UNITSIZE = 4 KiB, const.h:26) of
