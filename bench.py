@@ -165,9 +165,14 @@ def run_device(args):
     B = len(stripes)
     mat = ec.coding_matrix(k, m)
     g = torch.Generator(device="cuda").manual_seed(0xC0C70002 + rank)
-    data = [torch.randint(0, 256, (arena,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
-    parity = [torch.empty(arena, dtype=torch.uint8, device="cuda") for _ in range(m)]
-    out = [torch.zeros(arena, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    # the K data, M parity and K rebuilt arenas, carved from one allocation at the
+    # odd-4 KiB stride of cec_arenas_alloc (HBM channel layout)
+    arenas = ec.arena_tensors(k + m + k, arena)
+    data, parity, out = arenas[:k], arenas[k:k + m], arenas[k + m:]
+    for t in data:
+        t.random_(0, 256, generator=g)
+    for t in out:
+        t.zero_()
     masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
              for p in range(m) for j in range(k)]
     enc_plan = ec.Plan([(o, 0, ln, 0) for o, ln in stripes])

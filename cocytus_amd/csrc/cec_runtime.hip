@@ -390,6 +390,34 @@ static int check_code(int k, int m, const int *matrix) {
 
 #define MATRIX(x, y) matrix[(x) * k + (y)]
 
+// ============================================================== arena layout
+CEC_API size_t cec_arena_stride(size_t bytes) {
+    size_t pages = (bytes + kTile - 1) / kTile;
+    if (pages % 2 == 0) ++pages;  // odd number of 4 KiB pages between arena bases
+    return pages * kTile;
+}
+
+CEC_API int cec_arenas_alloc(int count, size_t bytes, uint8_t **arenas, void **slab) {
+    if (count < 1 || !arenas || !slab) return fail(CEC_EINVAL, "cec_arenas_alloc: bad args");
+    *slab = nullptr;
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    const size_t stride = cec_arena_stride(bytes);
+    uint8_t *base = nullptr;
+    if (hipMalloc(&base, stride * static_cast<size_t>(count)) != hipSuccess) {
+        (void)hipGetLastError();
+        return fail(CEC_ENOMEM, "cec_arenas_alloc: %d x %zu bytes", count, stride);
+    }
+    for (int i = 0; i < count; ++i) arenas[i] = base + static_cast<size_t>(i) * stride;
+    *slab = base;
+    return CEC_OK;
+}
+
+CEC_API int cec_arenas_free(void *slab) {
+    if (slab) HIP_TRY(hipFree(slab));
+    return CEC_OK;
+}
+
 // ============================================================== runtime API
 CEC_API const char *cec_version(void) { return "cocytus_ec 0.1 (gfx950)"; }
 CEC_API const char *cec_last_error(void) { return g_err; }

@@ -96,6 +96,9 @@ _SIGS = {
     "cec_solve": ([_i, _i, _ip, _u32, _pp, _pp, _vp, _vp], _i),
     "cec_decode": ([_i, _i, _ip, ctypes.POINTER(_u32), _i, _pp, _pp, _vp, _vp], _i),
     "cec_recovery_mask": ([_i, _i, _i, _ip], _u32),
+    "cec_arena_stride": ([ctypes.c_size_t], ctypes.c_size_t),
+    "cec_arenas_alloc": ([_i, ctypes.c_size_t, _pp, ctypes.POINTER(_vp)], _i),
+    "cec_arenas_free": ([_vp], _i),
     "cec_drainer_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, ctypes.c_size_t], _i),
     "cec_drainer_destroy": ([_vp], _i),
     "cec_drainer_apply": ([_vp, ctypes.POINTER(HostUpdate), _i, _vp, _vp], _i),
@@ -216,6 +219,21 @@ def set_engine(engine: int) -> None:
 
 def get_engine() -> int:
     return lib().cec_get_engine()
+
+
+def arena_stride(nbytes: int) -> int:
+    """cec_arena_stride: the HBM-friendly distance between arena bases (odd x 4 KiB)."""
+    return int(lib().cec_arena_stride(nbytes))
+
+
+def arena_tensors(count: int, nbytes: int, device="cuda"):
+    """count uint8 torch views of nbytes each, carved from one allocation at
+    cec_arena_stride(nbytes) -- the layout of cec_arenas_alloc, owned by torch."""
+    import torch
+
+    stride = arena_stride(nbytes)
+    slab = torch.empty(stride * count, dtype=torch.uint8, device=device)
+    return [slab[i * stride:i * stride + nbytes] for i in range(count)]
 
 
 class Plan:

@@ -601,6 +601,38 @@ def test_dropin_reentrant_threads(gpu, tmp_path):
     assert "0 mismatches" in out
 
 
+def test_arena_allocator(gpu, oracle):
+    """cec_arenas_alloc: count arenas at an odd-4 KiB stride, usable by every op."""
+    import ctypes
+
+    torch, ec = gpu
+    for nbytes, want in [(1, 4096), (4096, 4096), (8192, 12288), (256 << 20, (256 << 20) + 4096)]:
+        assert ec.arena_stride(nbytes) == want
+    k, m, n = 3, 2, 3 * 4096
+    arr = (ctypes.c_void_p * (k + m))()
+    slab = ctypes.c_void_p()
+    assert ec.lib().cec_arenas_alloc(k + m, n, arr, ctypes.byref(slab)) == 0
+    stride = ec.arena_stride(n)
+    assert [arr[i] - arr[0] for i in range(k + m)] == [i * stride for i in range(k + m)]
+    host = [oracle.splitmix_bytes(70 + j, n) for j in range(k)]
+    for j in range(k):
+        src = to_dev(torch, host[j])
+        ec.region_multiply(src, 1, n, arr[j], 0)  # copy into arena j
+    mat = ec.coding_matrix(k, m)
+    ec.encode_region(k, m, mat, [arr[j] for j in range(k)], [arr[k + p] for p in range(m)], n)
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, host)
+    for p in range(m):
+        got = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ec.region_multiply(arr[k + p], 1, n, got, 0)
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(got), exp[p])
+    assert ec.lib().cec_arenas_free(slab) == 0
+    views = ec.arena_tensors(4, 100)
+    assert all(v.numel() == 100 for v in views)
+    assert views[1].data_ptr() - views[0].data_ptr() == 4096
+
+
 def test_graph_capture_replay(gpu, oracle):
     """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
     bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
