@@ -35,6 +35,9 @@ namespace cec {
 
 constexpr int kTile = 4096;      // bytes per tile = kBlock lanes x 16 B
 constexpr int kBlock = 256;
+constexpr int kBlockLog2 = 8;
+constexpr uint64_t kLineBytes = 128;  // L2 / HBM line
+static_assert(kBlock == 1 << kBlockLog2, "kBlock must be a power of two");
 constexpr int kMaxStreams = 48;  // 16 data + 8 parity + 16 recovered + staging/diff ...
 constexpr int kPatN = 16;        // inputs per pattern (k <= CEC_MAX_K)
 constexpr int kPatL = 4;         // outputs per launch pattern (host splits more)
@@ -71,7 +74,7 @@ struct CombineArgs {
     const Pattern *patterns;
     uint64_t implicit_len;
     uint32_t n_tiles;
-    uint32_t pad;
+    uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
 };
 
 #define CEC_CONST __attribute__((address_space(4)))
@@ -253,13 +256,19 @@ __device__ inline void compute_chunk(const CEC_CONST Pattern *P, int n_in, int n
 //   0 none, 1 all, 2 all but the last (diff-update + install), 3 per pattern.
 enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 
+// A workgroup covers 1 / 2^split_shift of a tile (blockDim = kBlock >> split_shift):
+// work item g is tile g >> split_shift, part g & (2^split_shift - 1).
 template <int NT, int LT, class Eng, int kAcc, bool kExact>
 __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
     __shared__ uint32_t lds[Eng::kLdsWords];
     Eng::setup(lds);
-    const uint32_t lane = threadIdx.x;
+    const uint32_t sh = a.split_shift;
+    const uint64_t n_work = static_cast<uint64_t>(a.n_tiles) << sh;
 
-    for (uint32_t t = blockIdx.x; t < a.n_tiles; t += gridDim.x) {
+    for (uint64_t g = blockIdx.x; g < n_work; g += gridDim.x) {
+        const uint32_t t = static_cast<uint32_t>(g >> sh);
+        const uint32_t part = static_cast<uint32_t>(g) & ((1u << sh) - 1u);
+        const uint32_t lane = (part << (kBlockLog2 - sh)) + threadIdx.x;
         const TileRef tr = load_tile(a, t);
         const CEC_CONST Pattern *P = as_const(a.patterns) + tr.pattern;
         const int n_in = kExact ? NT : P->n_in;

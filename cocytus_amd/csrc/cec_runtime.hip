@@ -145,8 +145,8 @@ static void set_coef(Pattern &p, int l, int i, int c, int engine) {
 // ============================================================== launch
 template <int NT, int LT, class Eng, int kAcc, bool kExact>
 static void launch_k(const CombineArgs &a, int grid, hipStream_t s) {
-    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid), dim3(kBlock), 0,
-                       s, a);
+    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid),
+                       dim3(kBlock >> a.split_shift), 0, s, a);
 }
 
 // Exact-shape kernels for the hot ops: encode / decode / residual / solve (no RMW,
@@ -217,6 +217,7 @@ struct cec_plan {
     int64_t n_tiles = 0;
     uint64_t total = 0;
     bool overlap = false;
+    bool aligned_full = false;  // every tile a full kTile at 128-B aligned off / src_off
     Tile *d_tiles = nullptr;
     std::vector<cec_extent> h_ext;  // validation of per-op pattern indices
     std::vector<Tile> h_tiles;      // kept alive for the async upload
@@ -244,6 +245,9 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
         return fail(CEC_EINVAL, "cec_plan_create: more than 2^32 tiles");
     }
     p->n_tiles = static_cast<int64_t>(p->h_tiles.size());
+    p->aligned_full = std::all_of(p->h_tiles.begin(), p->h_tiles.end(), [](const Tile &t) {
+        return t.len == kTile && ((t.off | t.src_off) & (kLineBytes - 1)) == 0;
+    });
     {   // overlap of [off, off+len) among non-empty extents
         std::vector<std::pair<uint64_t, uint64_t>> r;
         r.reserve(n);
@@ -283,6 +287,23 @@ CEC_API int cec_plan_num_extents(const cec_plan *p) { return p ? p->n_ext : 0; }
 CEC_API int64_t cec_plan_num_tiles(const cec_plan *p) { return p ? p->n_tiles : 0; }
 CEC_API uint64_t cec_plan_total_bytes(const cec_plan *p) { return p ? p->total : 0; }
 
+// Workgroups per tile (log2).  Full tiles on 128-B lines stream fastest as four
+// 64-lane workgroups (finer dispatch, every wave equal work); ragged or unaligned
+// tiles keep one 256-lane workgroup per tile, since splitting them multiplies the
+// partial-line writes shared between workgroups (measured: DESIGN.md section 4).
+// CEC_SPLIT_SHIFT=0..2 pins the choice for measurement.
+static uint32_t split_shift_for(const Streams &st, const cec_plan *plan) {
+    static const int forced = [] {
+        const char *e = getenv("CEC_SPLIT_SHIFT");
+        return e && *e ? std::min(2, std::max(0, atoi(e))) : -1;
+    }();
+    if (forced >= 0) return static_cast<uint32_t>(forced);
+    uintptr_t mis = 0;
+    for (int i = 0; i < kMaxStreams; ++i) mis |= reinterpret_cast<uintptr_t>(st.base[i]);
+    const bool full = plan ? plan->aligned_full : true;
+    return full && (mis & (kLineBytes - 1)) == 0 ? 2u : 0u;
+}
+
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const cec_plan *plan, uint64_t implicit_len, hipStream_t stream) {
     CombineArgs a;
@@ -315,8 +336,9 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     // grid-stride grid: DESIGN.md).  LDS: persistent grid, so the per-workgroup
     // table staging is amortised over many tiles.
     const bool lds = g_engine.load() == CEC_ENGINE_LDS;
+    a.split_shift = lds ? 0 : split_shift_for(st, plan);
     const uint64_t max_grid = lds ? static_cast<uint64_t>(g_dev[dev].cus) * 8 : 0x7FFFFFFFull;
-    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles, max_grid));
+    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, max_grid));
     int en, el, eacc;
     const bool exact = exact_shape(pats, &en, &el, &eacc) &&
                        (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, stream)

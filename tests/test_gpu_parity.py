@@ -633,6 +633,17 @@ def test_arena_allocator(gpu, oracle):
     assert views[1].data_ptr() - views[0].data_ptr() == 4096
 
 
+@pytest.mark.parametrize("shift", [0, 1, 2])
+def test_forced_split_shift(gpu, oracle, shift):
+    """Every workgroups-per-tile choice (1, 2, 4) is bit-exact on aligned, ragged and
+    misaligned tiles, not only the one the automatic rule picks (cec_runtime.hip
+    split_shift_for).  Child process: the library reads CEC_SPLIT_SHIFT once."""
+    env = dict(os.environ, CEC_SPLIT_SHIFT=str(shift))
+    r = subprocess.run(["python", os.path.join(ROOT, "tests", "split_case.py")], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_graph_capture_replay(gpu, oracle):
     """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
     bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
