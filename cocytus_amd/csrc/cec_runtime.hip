@@ -211,13 +211,39 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
                        const cec_plan *plan, uint64_t implicit_len, hipStream_t stream);
 
 // ============================================================== plans
+// Tiles of one extent end on 4 KiB boundaries of the arena offset, so interior
+// tiles cover whole 128-B lines and only an extent's first / last tile shares a line
+// with a neighbouring workgroup (ecalloc packs values at 16-B granularity; tiling
+// from each value's start measured 4 % slower on the mixed workload).
+static inline size_t tiles_of(uint64_t off, uint32_t len) {
+    return len ? static_cast<size_t>((off % kTile + len + kTile - 1) / kTile) : 0;
+}
+static inline size_t append_tiles(Tile *t, uint64_t off, uint64_t src_off, uint32_t len,
+                                  uint32_t pattern) {
+    size_t n = 0;
+    for (uint32_t o = 0; o < len;) {
+        const uint32_t phase = static_cast<uint32_t>((off + o) % kTile);
+        const uint32_t step = std::min<uint32_t>(kTile - phase, len - o);
+        t[n++] = Tile{off + o, src_off + o, step, pattern};
+        o += step;
+    }
+    return n;
+}
+// Full tiles whose arena offset sits on a 128-B line (the written side: a line
+// written by two workgroups costs more than one read by two).
+static inline int64_t count_line_tiles(const Tile *t, size_t n) {
+    int64_t c = 0;
+    for (size_t i = 0; i < n; ++i) c += t[i].len == kTile && (t[i].off & (kLineBytes - 1)) == 0;
+    return c;
+}
+
 struct cec_plan {
     int device = -1;
     int n_ext = 0;
     int64_t n_tiles = 0;
     uint64_t total = 0;
     bool overlap = false;
-    bool aligned_full = false;  // every tile a full kTile at 128-B aligned off / src_off
+    int64_t n_line_tiles = 0;   // full kTile tiles at a 128-B aligned arena offset
     Tile *d_tiles = nullptr;
     std::vector<cec_extent> h_ext;  // validation of per-op pattern indices
     std::vector<Tile> h_tiles;      // kept alive for the async upload
@@ -233,21 +259,20 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
     p->device = dev;
     p->n_ext = n;
     p->h_ext.assign(ext, ext + n);
+    size_t total_tiles = 0;
+    for (int e = 0; e < n; ++e) total_tiles += tiles_of(ext[e].off, ext[e].len);
+    p->h_tiles.resize(total_tiles);
+    size_t nt = 0;
     for (int e = 0; e < n; ++e) {
-        const uint32_t len = ext[e].len;
-        p->total += len;
-        for (uint32_t o = 0; o < len; o += kTile)
-            p->h_tiles.push_back(Tile{ext[e].off + o, ext[e].src_off + o,
-                                      std::min<uint32_t>(kTile, len - o), ext[e].pattern});
+        p->total += ext[e].len;
+        nt += append_tiles(p->h_tiles.data() + nt, ext[e].off, ext[e].src_off, ext[e].len, ext[e].pattern);
     }
     if (p->h_tiles.size() > 0xFFFFFFFFull) {
         delete p;
         return fail(CEC_EINVAL, "cec_plan_create: more than 2^32 tiles");
     }
     p->n_tiles = static_cast<int64_t>(p->h_tiles.size());
-    p->aligned_full = std::all_of(p->h_tiles.begin(), p->h_tiles.end(), [](const Tile &t) {
-        return t.len == kTile && ((t.off | t.src_off) & (kLineBytes - 1)) == 0;
-    });
+    p->n_line_tiles = count_line_tiles(p->h_tiles.data(), p->h_tiles.size());
     {   // overlap of [off, off+len) among non-empty extents
         std::vector<std::pair<uint64_t, uint64_t>> r;
         r.reserve(n);
@@ -288,10 +313,10 @@ CEC_API int64_t cec_plan_num_tiles(const cec_plan *p) { return p ? p->n_tiles : 
 CEC_API uint64_t cec_plan_total_bytes(const cec_plan *p) { return p ? p->total : 0; }
 
 // Workgroups per tile (log2).  Full tiles on 128-B lines stream fastest as four
-// 64-lane workgroups (finer dispatch, every wave equal work); ragged or unaligned
-// tiles keep one 256-lane workgroup per tile, since splitting them multiplies the
-// partial-line writes shared between workgroups (measured: DESIGN.md section 4).
-// CEC_SPLIT_SHIFT=0..2 pins the choice for measurement.
+// 64-lane workgroups (finer dispatch, every wave equal work).  A plan that is mostly
+// small or line-misaligned tiles keeps one 256-lane workgroup per tile: splitting
+// those multiplies empty workgroups and partial lines written by two workgroups
+// (measured: DESIGN.md section 4).  CEC_SPLIT_SHIFT=0..2 pins the choice.
 static uint32_t split_shift_for(const Streams &st, const cec_plan *plan) {
     static const int forced = [] {
         const char *e = getenv("CEC_SPLIT_SHIFT");
@@ -300,7 +325,7 @@ static uint32_t split_shift_for(const Streams &st, const cec_plan *plan) {
     if (forced >= 0) return static_cast<uint32_t>(forced);
     uintptr_t mis = 0;
     for (int i = 0; i < kMaxStreams; ++i) mis |= reinterpret_cast<uintptr_t>(st.base[i]);
-    const bool full = plan ? plan->aligned_full : true;
+    const bool full = plan ? plan->n_line_tiles * 4 >= plan->n_tiles * 3 : true;
     return full && (mis & (kLineBytes - 1)) == 0 ? 2u : 0u;
 }
 
