@@ -74,6 +74,32 @@ __global__ __launch_bounds__(BLOCK) void k_v(P5 p, uint32_t ntiles) {
     }
 }
 
+// CombineArgs-like kernarg: 48 base pointers selected by per-launch stream ids.
+struct Big {
+    uint8_t *base[48];
+    int ids[8];
+};
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_big(Big a) {
+    const uint64_t o = (uint64_t)blockIdx.x * (BLOCK * 16) + threadIdx.x * 16;
+    const u32x4 x0 = ldn(a.base[a.ids[0]], o), x1 = ldn(a.base[a.ids[1]], o), x2 = ldn(a.base[a.ids[2]], o);
+    u32x4 x = x0 ^ x1 ^ x2;
+    stn<true>(a.base[a.ids[3]], o, x);
+    x.x ^= 0x1D;
+    stn<true>(a.base[a.ids[4]], o, x);
+}
+// the same block read from ordinary (cacheable) device memory through one pointer
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_ind(const Big *ap) {
+    const __attribute__((address_space(4))) Big *a = (const __attribute__((address_space(4))) Big *)(uintptr_t)ap;
+    const uint64_t o = (uint64_t)blockIdx.x * (BLOCK * 16) + threadIdx.x * 16;
+    const u32x4 x0 = ldn(a->base[a->ids[0]], o), x1 = ldn(a->base[a->ids[1]], o), x2 = ldn(a->base[a->ids[2]], o);
+    u32x4 x = x0 ^ x1 ^ x2;
+    stn<true>(a->base[a->ids[3]], o, x);
+    x.x ^= 0x1D;
+    stn<true>(a->base[a->ids[4]], o, x);
+}
+
 int main() {
     const uint64_t L = 256ull << 20;
     const uint64_t stride = L + 4096;  // cec_arena_stride(L)
@@ -82,6 +108,12 @@ int main() {
     for (int i = 0; i < 5; ++i) hipLaunchKernelGGL(k_fill, 4096, 256, 0, 0, (uint64_t *)(slab + i * stride), L / 8, 77ull + i);
     CK(hipDeviceSynchronize());
     P5 p{slab, slab + stride, slab + 2 * stride, slab + 3 * stride, slab + 4 * stride};
+    Big big{};
+    for (int i = 0; i < 48; ++i) big.base[i] = slab + (i % 5) * stride;
+    for (int i = 0; i < 5; ++i) big.ids[i] = 5 * (i + 2) + i;  // base[id] is arena id % 5 = i
+    Big *dbig;
+    CK(hipMalloc(&dbig, sizeof(Big)));
+    CK(hipMemcpy(dbig, &big, sizeof(Big), hipMemcpyHostToDevice));
     struct V {
         const char *name;
         int id;
@@ -101,6 +133,10 @@ int main() {
         {"64 thr x 2 chunks (2 KiB/WG) nt", 11},
         {"128 thr x 1 chunk (2 KiB/WG) plain", 12},
         {"192 thr x 1 chunk (3 KiB/WG) nt", 13},
+        {"64 thr, 400-B kernarg, dynamic base index", 14},
+        {"64 thr, args in device memory (1 ptr kernarg)", 15},
+        {"256 thr, 400-B kernarg, dynamic base index", 16},
+        {"256 thr, args in device memory", 17},
     };
     auto launch = [&](int id) {
         const uint32_t t4 = L / 4096;
@@ -118,6 +154,10 @@ int main() {
         case 10: hipLaunchKernelGGL((k_v<64, 1, false, true>), t4 * 4, 64, 0, 0, p, t4 * 4); break;
         case 11: hipLaunchKernelGGL((k_v<64, 2, false, true>), t4 * 2, 64, 0, 0, p, t4 * 2); break;
         case 12: hipLaunchKernelGGL((k_v<128, 1, false, false>), t4 * 2, 128, 0, 0, p, t4 * 2); break;
+        case 14: hipLaunchKernelGGL((k_big<64>), t4 * 4, 64, 0, 0, big); break;
+        case 15: hipLaunchKernelGGL((k_ind<64>), t4 * 4, 64, 0, 0, (const Big *)dbig); break;
+        case 16: hipLaunchKernelGGL((k_big<256>), t4, 256, 0, 0, big); break;
+        case 17: hipLaunchKernelGGL((k_ind<256>), t4, 256, 0, 0, (const Big *)dbig); break;
         case 13: hipLaunchKernelGGL((k_v<192, 1, false, true>), (uint32_t)(L / 3072), 192, 0, 0, p, (uint32_t)(L / 3072)); break;
         }
     };

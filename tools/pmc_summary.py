@@ -22,7 +22,13 @@ ALGO = {  # algorithmic bytes per launch: (encode, decode)
     "rs42_64k": ((4 + 2) * 65536 * 16384, (4 + 1) * 65536 * 16384),
     "rs32_1m": ((3 + 2) * (1 << 20) * 1024, (3 + 1) * (1 << 20) * 1024),
 }
-SHAPES = {"rs32_4k": ("<3, 2,", "<3, 1,"), "rs42_64k": ("<4, 2,", "<4, 1,"), "rs32_1m": ("<3, 2,", "<3, 1,")}
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402  (layout() of the mixed workload; no torch at import)
+
+_MIXED = sum(n for _, n in bench.layout("rs32_mixed")[0])
+ALGO["rs32_mixed"] = ((3 + 2) * _MIXED, (3 + 1) * _MIXED)
+SHAPES = {"rs32_4k": ("<3, 2,", "<3, 1,"), "rs42_64k": ("<4, 2,", "<4, 1,"), "rs32_1m": ("<3, 2,", "<3, 1,"),
+          "rs32_mixed": ("<3, 2,", "<3, 1,")}
 
 
 def one(path_glob):

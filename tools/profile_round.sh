@@ -11,7 +11,7 @@ OUT=$R/gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
 ARGS="--steps 10 --warmup 2 --no-cpu-baseline"
 cd /tmp && export TMPDIR=/tmp
-for W in rs32_4k rs42_64k rs32_1m; do
+for W in ${PROF_WORKLOADS:-rs32_4k rs32_mixed rs42_64k rs32_1m}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$W" -o run --output-format csv \
       -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_trace_$W.log" 2>&1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch_$W" -o run --output-format csv \

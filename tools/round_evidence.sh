@@ -1,7 +1,8 @@
 #!/bin/bash
 # tools/round_evidence.sh ROUND -- every measurement DESIGN.md quotes, on one box, one call
 # (run ON the GPU box through gpurun).  Results land in gpurun_out/evidence_ROUND/;
-# copy what is quoted into profiles/ (tools/collect_evidence.py does it here).
+# copy what is quoted into profiles/r01_evidence/ here (cp gpurun_out/evidence_ROUND/{*.jsonl,hbm_mix.txt}),
+# and run tools/pmc_summary.py on the merged gpurun_out/prof_ROUND.
 set -euo pipefail
 ROUND=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -19,5 +20,5 @@ $B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/ben
 $B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"
 timeout -k 10 200 tools/hbm_mix.bin    > "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
-bash tools/profile_round.sh "$ROUND"   > "$OUT/profile.log" 2>&1
+[ -n "${EVID_NO_PROF:-}" ] || bash tools/profile_round.sh "$ROUND" > "$OUT/profile.log" 2>&1
 echo done > "$OUT/DONE"
