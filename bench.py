@@ -107,7 +107,7 @@ def cpu_baseline(k, m, n, budget_s):
     threads = max(1, min(threads, 16))
     stripes = max(threads, (64 << 20) // n)  # 64 MiB per shard: larger than the host LLC
     t1 = pyoracle.bench_encode_decode(k, m, n, stripes, threads, 1, True)
-    reps = max(1, min(200, int(budget_s / max(t1 * threads, 1e-6))))
+    reps = max(1, min(2000, int(budget_s / max(t1 * threads, 1e-6))))
     t = pyoracle.bench_encode_decode(k, m, n, stripes, threads, reps, True)
     payload = (k + 1) * n * stripes * reps
     return {

@@ -21,8 +21,9 @@
 //   * GF multiply by a uniform coefficient c on 4 packed bytes:
 //       PERM engine: c*x = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6], three v_perm_b32
 //                    byte lookups per dword (tables are 8 bytes: two SGPRs);
-//       LDS engine : 256-entry log / antilog tables staged in LDS,
-//                    exp[log x + log c] with a zero sentinel (the north-star form);
+//       LDS engine : 256-entry product rows c*x = exp[log x + log c], one per
+//                    coefficient of the tile's pattern, built from the log / antilog
+//                    tables and staged in LDS per workgroup: one ds_read_u8 per byte;
 //     no MFMA: this is byte-field arithmetic, HBM-bound.
 #pragma once
 
@@ -54,9 +55,10 @@ struct alignas(16) Pattern {
     int32_t out_stream[kPatL];
     int32_t out_src[kPatL];
     int32_t out_mode[kPatL];      // kModeWrite / kModeXor
-    int32_t pad[2];
+    int32_t lds_rows;             // LDS engine: product rows this pattern stages ...
+    int32_t lds_row_base;         // ... starting at row lds_row_base of CombineArgs::rows
     int32_t coef[kPatL][kPatN];
-    uint32_t tab[kPatL][kPatN][5];  // PERM: PermTab; LDS: tab[..][0] = log(coef)
+    uint32_t tab[kPatL][kPatN][5];  // PERM: PermTab; LDS: tab[..][0] = LDS byte offset of the row
 };
 
 // One tile of the work-list: a <= 4 KiB piece of one extent, same layout as
@@ -72,6 +74,7 @@ struct CombineArgs {
     uint8_t *base[kMaxStreams];
     const Tile *tiles;       // NULL: implicit region [0, implicit_len), pattern 0
     const Pattern *patterns;
+    const uint8_t *rows;     // LDS engine: 256-B product rows (c*x for x = 0..255)
     uint64_t implicit_len;
     uint32_t n_tiles;
     uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
@@ -114,16 +117,15 @@ __device__ inline void st8(uint8_t *base, uint32_t off, uint32_t v) {
 
 // ---------------------------------------------------------------- engines
 struct PermEngine {
-    static constexpr int kLdsWords = 1;
+    static constexpr bool kStaged = false;
     struct Sel {
         uint32_t s0, s1, s2;
     };
-    __device__ static void setup(uint32_t *) {}
-    __device__ static inline Sel sel(uint32_t x, const uint32_t *) {
+    __device__ static inline Sel sel(uint32_t x) {
         return Sel{x & 0x07070707u, (x >> 3) & 0x07070707u, (x >> 6) & 0x03030303u};
     }
     __device__ static inline uint32_t mul(const Sel &s, const CEC_CONST uint32_t *t,
-                                          const uint32_t *) {
+                                          const uint8_t *) {
         const uint32_t a = __builtin_amdgcn_perm(t[1], t[0], s.s0);
         const uint32_t b = __builtin_amdgcn_perm(t[3], t[2], s.s1);
         const uint32_t c = __builtin_amdgcn_perm(t[4], t[4], s.s2);
@@ -131,37 +133,23 @@ struct PermEngine {
     }
 };
 
-// LDS layout (uint32 words): [0, 128) log as uint16[256] (log 0 -> 512 sentinel);
-// [128, 384) antilog as uint8[1024]: exp[i] = 2^(i mod 255) for i < 510, 0 above.
+// One 256-B row per non-trivial coefficient of the tile's pattern, row_c[x] = c*x
+// (row_c[0] = 0: no zero sentinel).  A ds_read_u8 of a 64-dword row has at most two
+// distinct dwords per bank (32 banks for byte / dword reads), and lanes that hit the
+// same dword broadcast, so a random lookup costs <= 2 LDS cycles per 32-lane group.
 struct LdsEngine {
-    static constexpr int kLdsWords = 384;
+    static constexpr bool kStaged = true;
     struct Sel {
-        uint32_t l01, l23;  // log of the 4 bytes, 16 bits each
+        uint32_t b0, b1, b2, b3;
     };
-    __device__ static void setup(uint32_t *lds) {
-        uint16_t *lg = reinterpret_cast<uint16_t *>(lds);
-        uint8_t *ex = reinterpret_cast<uint8_t *>(lds + 128);
-        for (int i = threadIdx.x; i < 256; i += blockDim.x)
-            lg[i] = i == 0 ? 512 : static_cast<uint16_t>(kGf.log[i]);
-        for (int i = threadIdx.x; i < 1024; i += blockDim.x)
-            ex[i] = i < 510 ? kGf.exp[i] : 0;
-        __syncthreads();
-    }
-    __device__ static inline Sel sel(uint32_t x, const uint32_t *lds) {
-        const uint16_t *lg = reinterpret_cast<const uint16_t *>(lds);
-        const uint32_t a = lg[x & 0xFF], b = lg[(x >> 8) & 0xFF];
-        const uint32_t c = lg[(x >> 16) & 0xFF], d = lg[x >> 24];
-        return Sel{a | (b << 16), c | (d << 16)};
+    __device__ static inline Sel sel(uint32_t x) {
+        return Sel{x & 0xFFu, (x >> 8) & 0xFFu, (x >> 16) & 0xFFu, x >> 24};
     }
     __device__ static inline uint32_t mul(const Sel &s, const CEC_CONST uint32_t *t,
-                                          const uint32_t *lds) {
-        const uint8_t *ex = reinterpret_cast<const uint8_t *>(lds + 128);
-        const uint32_t lc = t[0];
-        const uint32_t r0 = ex[(s.l01 & 0xFFFF) + lc];
-        const uint32_t r1 = ex[(s.l01 >> 16) + lc];
-        const uint32_t r2 = ex[(s.l23 & 0xFFFF) + lc];
-        const uint32_t r3 = ex[(s.l23 >> 16) + lc];
-        return r0 | (r1 << 8) | (r2 << 16) | (r3 << 24);
+                                          const uint8_t *lds) {
+        const uint8_t *row = lds + t[0];
+        return static_cast<uint32_t>(row[s.b0]) | (static_cast<uint32_t>(row[s.b1]) << 8) |
+               (static_cast<uint32_t>(row[s.b2]) << 16) | (static_cast<uint32_t>(row[s.b3]) << 24);
     }
 };
 
@@ -219,14 +207,14 @@ __device__ inline void scatter16(uint8_t *base, uint32_t off, uint32_t cnt, cons
 // acc[l] ^= sum_i coef[l][i] * x[i] on one 16-byte chunk of every stream.
 template <int NT, int LT, class Eng>
 __device__ inline void compute_chunk(const CEC_CONST Pattern *P, int n_in, int n_out,
-                                     const uint4 (&x)[NT], uint4 (&acc)[LT], const uint32_t *lds) {
+                                     const uint4 (&x)[NT], uint4 (&acc)[LT], const uint8_t *lds) {
 #pragma unroll
     for (int i = 0; i < NT; ++i) {
         if (i >= n_in) continue;
         const uint32_t xv[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
         typename Eng::Sel s[4];
 #pragma unroll
-        for (int w = 0; w < 4; ++w) s[w] = Eng::sel(xv[w], lds);
+        for (int w = 0; w < 4; ++w) s[w] = Eng::sel(xv[w]);
 #pragma unroll
         for (int l = 0; l < LT; ++l) {
             if (l >= n_out) continue;
@@ -260,8 +248,8 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 // work item g is tile g >> split_shift, part g & (2^split_shift - 1).
 template <int NT, int LT, class Eng, int kAcc, bool kExact>
 __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
-    __shared__ uint32_t lds[Eng::kLdsWords];
-    Eng::setup(lds);
+    extern __shared__ uint4 cec_lds_rows[];  // LDS engine: the pattern's product rows
+    const uint8_t *lds = reinterpret_cast<const uint8_t *>(cec_lds_rows);
     const uint32_t sh = a.split_shift;
     const uint64_t n_work = static_cast<uint64_t>(a.n_tiles) << sh;
 
@@ -274,6 +262,16 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
         const int n_in = kExact ? NT : P->n_in;
         const int n_out = kExact ? LT : P->n_out;
         if (!kExact && n_out == 0) continue;
+        if constexpr (Eng::kStaged) {
+            // Stage this pattern's rows (L2-resident, 256 B each; 512 B for an RS(3,2)
+            // encode).  The barrier before re-staging only matters when a workgroup
+            // walks several tiles (more than 2^31 work items).
+            if (g != blockIdx.x) __syncthreads();
+            const uint32_t nb = static_cast<uint32_t>(P->lds_rows) * 256u;
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
+            for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
+            __syncthreads();
+        }
         auto is_acc = [&](int l) -> bool {
             if constexpr (kAcc == kAccNone) return false;
             else if constexpr (kAcc == kAccAll) return true;

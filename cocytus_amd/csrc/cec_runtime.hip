@@ -107,8 +107,12 @@ struct PatternCache {
 };
 static PatternCache g_pcache[64];
 
-static int upload_patterns(int dev, const std::vector<Pattern> &pats, const Pattern **out) {
+// Patterns and the LDS engine's product rows are uploaded as one blob: rows follow
+// the patterns (16-B aligned: sizeof(Pattern) is a multiple of 16).
+static int upload_patterns(int dev, const std::vector<Pattern> &pats, const std::vector<uint8_t> &rows,
+                           const Pattern **out) {
     std::string key(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
+    key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
     PatternCache &c = g_pcache[dev];
     std::lock_guard<std::mutex> lk(c.mu);
     auto it = c.map.find(key);
@@ -134,29 +138,52 @@ static Pattern blank_pattern() {
 static void set_coef(Pattern &p, int l, int i, int c, int engine) {
     c &= 0xFF;
     p.coef[l][i] = static_cast<uint8_t>(c);
-    if (engine == CEC_ENGINE_LDS) {
-        p.tab[l][i][0] = c ? static_cast<uint32_t>(kGf.log[c]) : 0u;
-    } else {
+    if (engine != CEC_ENGINE_LDS) {
         const PermTab t = make_perm_tab(c);
         for (int w = 0; w < 5; ++w) p.tab[l][i][w] = t.w[w];
     }
 }
 
+// LDS engine: one 256-B product row per distinct coefficient c >= 2 of the pattern,
+// row_c[x] = exp[log x + log c] (0 for x = 0), appended to `rows`; the kernel stages
+// the pattern's rows into LDS and looks up one byte per byte (cec_kernels.hpp).
+static void assign_rows(Pattern &p, std::vector<uint8_t> &rows) {
+    int row_of[256];
+    for (int &r : row_of) r = -1;
+    const size_t base = rows.size() / 256;
+    int nr = 0;
+    for (int l = 0; l < p.n_out; ++l)
+        for (int i = 0; i < p.n_in; ++i) {
+            const int c = p.coef[l][i];
+            if (c < 2) continue;  // 0 and 1 are uniform branches, no table
+            if (row_of[c] < 0) {
+                row_of[c] = nr++;
+                for (int x = 0; x < 256; ++x)
+                    rows.push_back(x ? kGf.exp[kGf.log[x] + kGf.log[c]] : 0);
+            }
+            p.tab[l][i][0] = static_cast<uint32_t>(row_of[c]) * 256u;
+        }
+    p.lds_rows = nr;
+    p.lds_row_base = static_cast<int32_t>(base);
+}
+
 // ============================================================== launch
+// `lds`: dynamic LDS bytes of the launch (LDS engine: the largest pattern's rows).
 template <int NT, int LT, class Eng, int kAcc, bool kExact>
-static void launch_k(const CombineArgs &a, int grid, hipStream_t s) {
+static void launch_k(const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid),
-                       dim3(kBlock >> a.split_shift), 0, s, a);
+                       dim3(kBlock >> a.split_shift), Eng::kStaged ? lds : 0, s, a);
 }
 
 // Exact-shape kernels for the hot ops: encode / decode / residual / solve (no RMW,
 // up to 8 inputs x 4 outputs), parity apply and region multiply-XOR (1 x 1 RMW),
 // diff-update (2 inputs, M parity RMW outputs, optionally + install).
 template <class Eng>
-static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, hipStream_t s) {
+static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, size_t lds,
+                         hipStream_t s) {
 #define CEC_X(N, L, A)                                           \
     if (n == N && l == L && acc == A) {                          \
-        launch_k<N, L, Eng, A, true>(a, grid, s);                \
+        launch_k<N, L, Eng, A, true>(a, grid, lds, s);           \
         return true;                                             \
     }
 #define CEC_XL(N) CEC_X(N, 1, kAccNone) CEC_X(N, 2, kAccNone) CEC_X(N, 3, kAccNone) CEC_X(N, 4, kAccNone)
@@ -171,11 +198,11 @@ static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, 
 
 // Capacity kernels for every other shape (guarded, per-pattern counts and modes).
 template <class Eng>
-static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, hipStream_t s) {
+static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
 #define CEC_G(NT)                                                                    \
-    if (lt <= 1) launch_k<NT, 1, Eng, kAccRuntime, false>(a, grid, s);              \
-    else if (lt <= 2) launch_k<NT, 2, Eng, kAccRuntime, false>(a, grid, s);         \
-    else launch_k<NT, 4, Eng, kAccRuntime, false>(a, grid, s);
+    if (lt <= 1) launch_k<NT, 1, Eng, kAccRuntime, false>(a, grid, lds, s);          \
+    else if (lt <= 2) launch_k<NT, 2, Eng, kAccRuntime, false>(a, grid, lds, s);     \
+    else launch_k<NT, 4, Eng, kAccRuntime, false>(a, grid, lds, s);
     if (nt <= 2) { CEC_G(2) }
     else if (nt <= 4) { CEC_G(4) }
     else if (nt <= 8) { CEC_G(8) }
@@ -208,7 +235,8 @@ struct Streams {
 
 // One launch over a tile source (plan or implicit region) with a pattern set.
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
-                       const cec_plan *plan, uint64_t implicit_len, hipStream_t stream);
+                       const std::vector<uint8_t> &rows, const cec_plan *plan,
+                       uint64_t implicit_len, hipStream_t stream);
 
 // ============================================================== plans
 // Tiles of one extent end on 4 KiB boundaries of the arena offset, so interior
@@ -330,7 +358,8 @@ static uint32_t split_shift_for(const Streams &st, const cec_plan *plan) {
 }
 
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
-                       const cec_plan *plan, uint64_t implicit_len, hipStream_t stream) {
+                       const std::vector<uint8_t> &rows, const cec_plan *plan,
+                       uint64_t implicit_len, hipStream_t stream) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
     for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
@@ -353,24 +382,27 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     }
     if (lt == 0) return CEC_OK;
     const Pattern *dp = nullptr;
-    if (int r = upload_patterns(dev, pats, &dp)) return r;
+    if (int r = upload_patterns(dev, pats, rows, &dp)) return r;
     a.patterns = dp;
+    a.rows = reinterpret_cast<const uint8_t *>(dp + pats.size());
     a.n_tiles = static_cast<uint32_t>(n_tiles);
-    // PERM: one workgroup per tile, dispatched in tile order, so the set of tiles in
-    // flight is a contiguous window of the arenas (measured 5-12 % over a persistent
-    // grid-stride grid: DESIGN.md).  LDS: persistent grid, so the per-workgroup
-    // table staging is amortised over many tiles.
+    // One workgroup per (part of a) tile, dispatched in tile order, so the set of
+    // tiles in flight is a contiguous window of the arenas (measured 5-12 % over a
+    // persistent grid-stride grid: DESIGN.md).  The LDS engine stages its pattern's
+    // product rows per workgroup (512 B for an RS(3,2) encode, from L2).
     const bool lds = g_engine.load() == CEC_ENGINE_LDS;
-    a.split_shift = lds ? 0 : split_shift_for(st, plan);
-    const uint64_t max_grid = lds ? static_cast<uint64_t>(g_dev[dev].cus) * 8 : 0x7FFFFFFFull;
-    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, max_grid));
+    int max_rows = 0;
+    for (const Pattern &p : pats) max_rows = std::max(max_rows, p.lds_rows);
+    const size_t lds_bytes = static_cast<size_t>(max_rows) * 256;
+    a.split_shift = split_shift_for(st, plan);
+    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, 0x7FFFFFFFull));
     int en, el, eacc;
     const bool exact = exact_shape(pats, &en, &el, &eacc) &&
-                       (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, stream)
-                            : launch_exact<PermEngine>(en, el, eacc, a, grid, stream));
+                       (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, lds_bytes, stream)
+                            : launch_exact<PermEngine>(en, el, eacc, a, grid, 0, stream));
     if (!exact) {
-        if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, stream);
-        else launch_generic<PermEngine>(nt, lt, a, grid, stream);
+        if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, lds_bytes, stream);
+        else launch_generic<PermEngine>(nt, lt, a, grid, 0, stream);
     }
     HIP_TRY(hipGetLastError());
     return CEC_OK;
@@ -396,6 +428,7 @@ static int run_combos(int dev, const Streams &st, const std::vector<Combo> &comb
     const size_t groups = (max_out + kPatL - 1) / kPatL;
     for (size_t g = 0; g < groups; ++g) {
         std::vector<Pattern> pats;
+        std::vector<uint8_t> rows;
         pats.reserve(combos.size());
         for (const Combo &c : combos) {
             Pattern p = blank_pattern();
@@ -417,9 +450,10 @@ static int run_combos(int dev, const Streams &st, const std::vector<Combo> &comb
                 for (int i = 0; i < c.n_in; ++i) set_coef(p, no, i, q.coef[i], engine);
             }
             p.n_out = no;
+            if (engine == CEC_ENGINE_LDS) assign_rows(p, rows);
             pats.push_back(p);
         }
-        if (int r = run_combine(dev, st, pats, plan, implicit_len, stream)) return r;
+        if (int r = run_combine(dev, st, pats, rows, plan, implicit_len, stream)) return r;
     }
     return CEC_OK;
 }

@@ -64,8 +64,9 @@ typedef struct cec_extent {
 typedef struct cec_plan cec_plan;
 
 /* GF(2^8) engine used by the kernels.  Both are bit-exact; PERM (default) looks up
- * three 8-entry byte tables per coefficient with v_perm_b32 (pure VALU); LDS is the
- * 256-entry log / antilog tables staged in LDS (two ds_read_u8 per byte). */
+ * three 8-entry byte tables per coefficient with v_perm_b32 (pure VALU); LDS stages
+ * one 256-entry product row per coefficient, exp[log x + log c] built from the
+ * log / antilog tables, in LDS (one ds_read_u8 per byte). */
 typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1 } cec_engine;
 
 /* ---- runtime ---- */
