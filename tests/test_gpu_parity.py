@@ -682,7 +682,7 @@ def test_graph_capture_replay(gpu, oracle):
     dp.destroy()
 
 
-def test_edge_cases(gpu, oracle):
+def test_edge_cases(gpu, oracle, engine):
     """Empty plans and zero-length extents, k+m at the limit, bad masks / patterns."""
     torch, ec = gpu
     k, m = 16, 8  # CEC_MAX_K, CEC_MAX_M

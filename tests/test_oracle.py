@@ -245,3 +245,30 @@ def test_golden_recomputed_by_oracle(oracle):
             lost = [j for j in range(k) if not (mask >> j) & 1]
             for x, j in enumerate(lost):
                 assert np.array_equal(out[x], z[f"mask{mask}_lost{j}"])
+
+
+def test_oracle_vs_system_jerasure(oracle):
+    """Pin the oracle against a real Jerasure 2.x when the machine has one (SURVEY §8c:
+    'cross-checked against real libJerasure if the box has it').  This image has
+    none, so this skips and the oracle stays 'parity unpinned' (DESIGN.md §2)."""
+    from oracle import jerasure_probe
+
+    lib, where = jerasure_probe.load()
+    if lib is None:
+        pytest.skip(where)
+    for k, m in [(3, 2), (4, 2), (6, 3)]:
+        mat = jerasure_probe.matrix(lib, k, m)
+        assert mat == oracle.big_vandermonde(k + m, k), (k, m, where)
+        data = [oracle.splitmix_bytes(0xC0C70001 + j, 4096 + 7) for j in range(k)]
+        ref = jerasure_probe.encode(lib, mat, k, m, data)
+        ours = oracle.encode(mat, k, m, data)
+        for p in range(m):
+            assert np.array_equal(ref[p], ours[p]), (k, m, p, where)
+
+
+def test_jerasure_probe_rejects_the_shim():
+    """The probe must never return the repository's own libJerasure.so symlink."""
+    from oracle import jerasure_probe
+
+    for p in jerasure_probe.candidates():
+        assert not os.path.realpath(p).startswith(jerasure_probe.ROOT + os.sep), p
