@@ -716,3 +716,84 @@ def test_edge_cases(gpu, oracle, engine):
             ec.decode(3, 2, ec.coding_matrix(3, 2), [0b00011, 0b0111], ddev[:5], odev[:3], plan)
     with pytest.raises(ec.CecError):
         ec.encode_region(17, 2, [1] * 19 * 17, ddev[:17] + [ddev[0]], pdev[:2], 16)
+
+
+# ------------------------------------------------------------------ randomized sweep
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_random_plans(gpu, oracle, seed):
+    """Random code, engine, extent sizes / offsets and arena base misalignment, for
+    encode, diff-update and decode in one pass; every byte checked against the oracle."""
+    torch, ec = gpu
+    rng = np.random.default_rng(0xF022 + seed)
+    k = int(rng.integers(2, 9))
+    m = int(rng.integers(1, 5))
+    ec.set_engine(ec.CEC_ENGINE_LDS if seed % 2 else ec.CEC_ENGINE_PERM)
+    try:
+        mat = ec.coding_matrix(k, m)
+        kind = rng.choice(["small", "tiles", "large"])
+        hi = {"small": 300, "tiles": 9000, "large": 200000}[kind]
+        lens = [int(x) for x in rng.integers(0, hi, int(rng.integers(1, 40)))]
+        ext, arena_len, stage_len = make_extents(rng, lens, unaligned_every=int(rng.integers(0, 5)))
+        shift = int(rng.integers(0, 16)) if seed % 3 == 0 else 0  # misaligned arena bases
+
+        def dev(a):
+            buf = torch.zeros(a.size + shift, dtype=torch.uint8, device="cuda")
+            view = buf[shift:]
+            view.copy_(torch.from_numpy(np.ascontiguousarray(a)))
+            return view
+
+        data = [rng.integers(0, 256, arena_len, dtype=np.uint8) for _ in range(k)]
+        ddev = [dev(d) for d in data]
+        pdev = [dev(np.full(arena_len, SENT, np.uint8)) for _ in range(m)]
+        with ec.Plan([tuple(e) for e in ext]) as plan:
+            ec.encode(k, m, mat, ddev, pdev, plan)
+            torch.cuda.synchronize()
+        parity = [np.full(arena_len, SENT, np.uint8) for _ in range(m)]
+        for off, _, n, _ in ext:
+            if n:
+                ps = oracle.encode(mat, k, m, [d[off:off + n].copy() for d in data])
+                for p in range(m):
+                    parity[p][off:off + n] = ps[p]
+        for p in range(m):
+            assert np.array_equal(to_host(pdev[p]), parity[p]), ("encode", p)
+        # diff-update with install on a random source shard per extent
+        for e in ext:
+            e[3] = int(rng.integers(0, k))
+        staging = rng.integers(0, 256, stage_len, dtype=np.uint8)
+        with ec.Plan([tuple(e) for e in ext]) as plan:
+            ec.diff_update(k, m, mat, ddev, dev(staging), pdev, True, plan)
+            torch.cuda.synchronize()
+        for off, soff, n, j in ext:
+            if not n:
+                continue
+            old = data[j][off:off + n].copy()
+            pv = [p[off:off + n].copy() for p in parity]
+            oracle.diff_update(mat, k, m, j, old, staging[soff:soff + n].copy(), pv, True)
+            data[j][off:off + n] = old
+            for p in range(m):
+                parity[p][off:off + n] = pv[p]
+        for j in range(k):
+            assert np.array_equal(to_host(ddev[j]), data[j]), ("diff_update data", j)
+        for p in range(m):
+            assert np.array_equal(to_host(pdev[p]), parity[p]), ("diff_update parity", p)
+        # decode under a random mask per extent
+        masks = list(all_masks(k, m))
+        pick = rng.choice(len(masks), min(len(masks), 6), replace=False)
+        masks = [masks[int(i)] for i in pick]
+        for e in ext:
+            e[3] = int(rng.integers(0, len(masks)))
+        odev = [dev(np.full(arena_len, SENT, np.uint8)) for _ in range(k)]
+        with ec.Plan([tuple(e) for e in ext]) as plan:
+            ec.decode(k, m, mat, masks, ddev + pdev, odev, plan)
+            torch.cuda.synchronize()
+        out = [np.full(arena_len, SENT, np.uint8) for _ in range(k)]
+        for off, _, n, q in ext:
+            if not n:
+                continue
+            for j in range(k):
+                if not (masks[q] >> j) & 1:
+                    out[j][off:off + n] = data[j][off:off + n]
+        for j in range(k):
+            assert np.array_equal(to_host(odev[j]), out[j]), ("decode", j)
+    finally:
+        ec.set_engine(ec.CEC_ENGINE_PERM)
