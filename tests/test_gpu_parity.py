@@ -797,3 +797,63 @@ def test_fuzz_random_plans(gpu, oracle, seed):
             assert np.array_equal(to_host(odev[j]), out[j]), ("decode", j)
     finally:
         ec.set_engine(ec.CEC_ENGINE_PERM)
+
+
+# ------------------------------------------------------------------ reference allocator layout
+def test_reference_allocator_layout(gpu, oracle, engine):
+    """SETs placed by the reference's own allocator (tests/golden/ecalloc_layout.npz,
+    from /root/reference/ecalloc.c after churn): per-shard fused diff-update with
+    install, and the parity drain of the same diffs across shards (overlapping in the
+    parity arena, memcached.c:7704-7717), each equal to the reference's chain."""
+    torch, ec = gpu
+    z = np.load(os.path.join(ROOT, "tests", "golden", "ecalloc_layout.npz"))
+    sets = [tuple(int(x) for x in row) for row in z["sets"]]
+    k, m = int(z["k"]), 2
+    mat = ec.coding_matrix(k, m)
+    arena = ((max(a + n for _, a, n in sets) + 4095) // 4096) * 4096
+    rng = np.random.default_rng(0xA10)
+    data = [rng.integers(0, 256, arena, dtype=np.uint8) for _ in range(k)]  # stale bytes
+    parity = oracle.encode(mat, k, m, data)
+    news, soff, ext = [], 0, {j: [] for j in range(k)}
+    for j, a, n in sets:
+        news.append(rng.integers(0, 256, n, dtype=np.uint8))
+        ext[j].append((a, soff, n, j))
+        soff = (soff + n + 15) & ~15
+    staging = np.zeros(soff, np.uint8)
+    so_of = {}
+    for j in range(k):
+        for a, so, n, _ in ext[j]:
+            so_of[(j, a)] = so
+    for (j, a, n), v in zip(sets, news):
+        staging[so_of[(j, a)]:so_of[(j, a)] + n] = v
+    ddev = [to_dev(torch, d) for d in data]
+    pdev = [to_dev(torch, p) for p in parity]
+    sdev = to_dev(torch, staging)
+    p_drain = to_dev(torch, parity[1])
+    # the shipped diffs (new ^ stale old bytes at the fresh address, memcached.c:2673-2681)
+    diffs = [(oracle.set_diff(data[j][a:a + n].copy(), v), a, j) for (j, a, n), v in zip(sets, news)]
+    for j in range(k):  # one launch per shard: its SETs never overlap each other
+        with ec.Plan(ext[j]) as plan:
+            ec.diff_update(k, m, mat, ddev, sdev, pdev, True, plan)
+    with ec.Drainer(k, m, mat, k + 1, staging_bytes=8 << 20) as d:
+        launches = d.apply(diffs, p_drain)
+    torch.cuda.synchronize()
+    assert launches >= 2  # cross-shard overlaps need several waves
+    drained = parity[1].copy()
+    for d_, a, j in diffs:  # the parity's drain loop, one diff at a time
+        v = drained[a:a + d_.size].copy()
+        oracle.parity_apply(mat, k, k + 1, j, d_, v)
+        drained[a:a + d_.size] = v
+    assert np.array_equal(to_host(p_drain), drained)
+    for (j, a, n), v in zip(sets, news):  # the data-side chain, SET by SET
+        old = data[j][a:a + n].copy()
+        pv = [p[a:a + n].copy() for p in parity]
+        oracle.diff_update(mat, k, m, j, old, v, pv, True)
+        data[j][a:a + n] = old
+        for p in range(m):
+            parity[p][a:a + n] = pv[p]
+    for j in range(k):
+        assert np.array_equal(to_host(ddev[j]), data[j]), j
+    for p in range(m):
+        assert np.array_equal(to_host(pdev[p]), parity[p]), p
+    assert np.array_equal(drained, parity[1])  # drain == per-shard fused update

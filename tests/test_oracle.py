@@ -272,3 +272,35 @@ def test_jerasure_probe_rejects_the_shim():
 
     for p in jerasure_probe.candidates():
         assert not os.path.realpath(p).startswith(jerasure_probe.ROOT + os.sep), p
+
+
+def _ecalloc_fixture():
+    z = np.load(os.path.join(GOLDEN, "ecalloc_layout.npz"))
+    return [tuple(int(x) for x in row) for row in z["sets"]], int(z["seed"]), int(z["k"])
+
+
+def test_ecalloc_fixture_matches_reference():
+    """tests/golden/ecalloc_layout.npz is what the reference's own allocator
+    (/root/reference/ecalloc.c, built into oracle/_ref) hands out for that SET trace."""
+    from oracle import ecalloc_ref
+
+    if not ecalloc_ref.available():
+        pytest.skip("oracle/_ref/libecalloc_ref.so not built (needs /root/reference)")
+    sets, seed, k = _ecalloc_fixture()
+    assert ecalloc_ref.set_trace(seed, k) == sets
+
+
+def test_ecalloc_layout_contract():
+    """The address contract the kernels rely on: 16-B aligned
+    starts (ecalloc.c:176), no overlap within one shard's batch, and -- because each
+    lid has its own allocator -- overlaps ACROSS shards in the parity arena."""
+    sets, _, k = _ecalloc_fixture()
+    assert all(a % 16 == 0 for _, a, _ in sets)
+    cross = 0
+    for j in range(k):
+        r = sorted((a, a + n) for jj, a, n in sets if jj == j)
+        assert all(r[i][0] >= r[i - 1][1] for i in range(1, len(r))), j
+    allr = sorted((a, a + n, j) for j, a, n in sets)
+    for i in range(1, len(allr)):
+        cross += allr[i][0] < allr[i - 1][1]
+    assert cross > 0
