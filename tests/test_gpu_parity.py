@@ -857,3 +857,17 @@ def test_reference_allocator_layout(gpu, oracle, engine):
     for p in range(m):
         assert np.array_equal(to_host(pdev[p]), parity[p]), p
     assert np.array_equal(drained, parity[1])  # drain == per-shard fused update
+
+
+def test_reference_microbenchmark_on_shim(gpu):
+    """The reference's own micro-benchmark (microbenchmarks/galois_tp.c: one 512 MiB
+    galois_w08_region_multiply from malloc'd memory), compiled unmodified against the
+    shim's <galois.h> and linked -lJerasure (oracle/Makefile `ref`), runs to completion
+    on the GPU.  Skips where oracle/_ref was not built (no /root/reference)."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "galois_tp")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref/galois_tp not built")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    parts = r.stdout.split()
+    assert len(parts) == 4 and parts[1] == "s" and parts[3] == "ns", r.stdout
