@@ -112,6 +112,7 @@ _SIGS = {
     "cec_recovery_residual": ([_vp], _vp),
     "cec_recovery_bytes": ([_vp], ctypes.c_uint64),
     "cec_recovery_solve": ([_vp, _pp, _pp, _vp], _i),
+    "cec_recovery_finish": ([_vp, _i, _vp, _pp, _pp, _vp], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
     "cec_event_destroy": ([_vp], _i),
     "cec_event_record": ([_vp, _vp], _i),
@@ -432,6 +433,13 @@ class Recovery:
                                                      for i in range(self.k + self.m)])
         oo = (ctypes.c_void_p * self.k)(*[_host_or_dev(out.get(j)) or None for j in range(self.k)])
         _check(lib().cec_recovery_solve(self._h, pr, oo, _stream(stream)))
+
+    def finish(self, peer_lid: int, units, peer_residuals: dict, out: dict, stream=None) -> None:
+        """add_peer(peer_lid, units) + solve(peer_residuals, out) in one pipelined pass."""
+        pr = (ctypes.c_void_p * (self.k + self.m))(*[_host_or_dev(peer_residuals.get(i)) or None
+                                                     for i in range(self.k + self.m)])
+        oo = (ctypes.c_void_p * self.k)(*[_host_or_dev(out.get(j)) or None for j in range(self.k)])
+        _check(lib().cec_recovery_finish(self._h, peer_lid, _host_or_dev(units), pr, oo, _stream(stream)))
 
     def destroy(self) -> None:
         if self._h:

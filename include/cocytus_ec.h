@@ -239,6 +239,14 @@ uint64_t cec_recovery_bytes(const cec_recovery *r);
 int cec_recovery_solve(cec_recovery *leader, const void *const *peer_residuals,
                        void *const *out, void *stream);
 
+/* The last data peer and the leader solve (= cec_recovery_add_peer of that peer, then
+ * cec_recovery_solve; same bytes, same residual afterwards).  With device or pinned
+ * buffers it is ONE pass: the kernel reads the peer's bytes and writes the rebuilt
+ * bytes (over PCIe in both directions at once for pinned host memory).  Pageable
+ * buffers take the two-step path.  EINVAL if peer is not the last data peer. */
+int cec_recovery_finish(cec_recovery *leader, int peer_lid, const void *units,
+                        const void *const *peer_residuals, void *const *out, void *stream);
+
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
 int cec_event_create(void **ev);
 int cec_event_destroy(void *ev);

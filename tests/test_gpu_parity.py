@@ -871,3 +871,95 @@ def test_reference_microbenchmark_on_shim(gpu):
     assert r.returncode == 0, r.stderr[-2000:]
     parts = r.stdout.split()
     assert len(parts) == 4 and parts[1] == "s" and parts[3] == "ns", r.stdout
+
+
+@pytest.mark.parametrize("kind", ["pageable", "pinned", "device", "pageable_in_device_out"])
+def test_recovery_finish_matches_two_step(gpu, oracle, kind):
+    """cec_recovery_finish (last peer + leader solve, pipelined in 16 MiB pieces) ==
+    add_peer + solve: same rebuilt bytes, same residual, for every buffer kind; with a
+    diff folded before the last peer (recovery.c:99-131)."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(sum(map(ord, kind)))
+    nunits = 9 * 1024 + 37  # 36 MiB + 37 units: three pieces, the last one partial
+    n = nunits * U
+    data = [rng.integers(0, 256, n, dtype=np.uint8) for _ in range(k)]
+    pdev = [to_dev(torch, p) for p in oracle.encode(mat, k, m, data)]
+    mask = oracle.recovery_mask(k, m, 4, [1, 0, 1, 1, 1])  # D1 lost, leader P1 (inverse 1/245)
+
+    def buf(a, what):
+        if what == "device":
+            return to_dev(torch, a)
+        if what == "pinned":
+            return torch.from_numpy(a.copy()).pin_memory()
+        return a.copy()
+
+    in_kind = {"pageable_in_device_out": "pageable"}.get(kind, kind)
+    out_kind = {"pageable_in_device_out": "device"}.get(kind, kind)
+    diff = rng.integers(0, 256, 5000, dtype=np.uint8)
+    outs, resid = [], []
+    for fused in (False, True):
+        with ec.Recovery(k, m, mat, 4, mask, 0, nunits - 1, pdev[1]) as rec:
+            rec.add_peer(0, buf(data[0], in_kind))
+            assert rec.fold_update(2, 4096 * 7 + 16, diff) >= 1  # peer 2 not yet applied
+            o = buf(np.zeros(n, np.uint8), out_kind)
+            if fused:
+                rec.finish(2, buf(data[2], in_kind), {}, {1: o})
+            else:
+                rec.add_peer(2, buf(data[2], in_kind))
+                rec.solve({}, {1: o})
+            assert rec.complete
+            torch.cuda.synchronize()
+            outs.append(o.cpu().numpy() if hasattr(o, "cpu") else o)
+            tmp = torch.empty(n, dtype=torch.uint8, device="cuda")
+            ec.region_multiply(rec.residual, 1, n, tmp, 0)
+            torch.cuda.synchronize()
+            resid.append(to_host(tmp))
+    assert np.array_equal(outs[1], outs[0])
+    assert np.array_equal(resid[1], resid[0])
+    # the folded diff makes the rebuilt bytes differ from data[1] exactly where the
+    # reference's would: D1' = D1 ^ inv * MATRIX(P1, D2) * diff over that piece
+    exp = data[1].copy()
+    v = np.zeros(5000, np.uint8)
+    oracle.region_multiply(diff, oracle.gf_mul(oracle.gf_div(1, mat[4 * k + 1]), mat[4 * k + 2]), v, 1)
+    exp[4096 * 7 + 16:4096 * 7 + 16 + 5000] ^= v
+    assert np.array_equal(outs[1], exp)
+
+
+@pytest.mark.parametrize("outs_kind", ["device", "one_pageable", "two_pageable"])
+def test_recovery_finish_double_loss(gpu, oracle, outs_kind):
+    """D0, D1 lost: P1 ships its residual; the leader P0 finishes with the last data peer
+    D2 and rebuilds both shards in the same pass."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    nunits = 4 * 1024 + 3
+    n = nunits * U
+    data = [oracle.splitmix_bytes(0xC0C70105 + j, n) for j in range(k)]
+    pdev = [to_dev(torch, p) for p in oracle.encode(mat, k, m, data)]
+    mask = 0b11100
+    with ec.Recovery(k, m, mat, 3, mask, 0, nunits - 1, pdev[0]) as r0, \
+         ec.Recovery(k, m, mat, 4, mask, 0, nunits - 1, pdev[1]) as r1:
+        r1.add_peer(2, data[2])
+        res1 = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ec.region_multiply(r1.residual, 1, n, res1, 0)
+        torch.cuda.synchronize()
+        res1_host = to_host(res1)
+        o0 = np.zeros(n, np.uint8) if outs_kind != "device" else torch.zeros(n, dtype=torch.uint8, device="cuda")
+        o1 = np.zeros(n, np.uint8) if outs_kind == "two_pageable" else torch.zeros(n, dtype=torch.uint8, device="cuda")
+        r0.finish(2, data[2], {4: res1_host}, {0: o0, 1: o1})
+        torch.cuda.synchronize()
+    got = [x.cpu().numpy() if hasattr(x, "cpu") else x for x in (o0, o1)]
+    assert np.array_equal(got[0], data[0]) and np.array_equal(got[1], data[1])
+
+
+def test_recovery_finish_rejects_early_peer(gpu, oracle):
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    p = torch.zeros(8 * 4096, dtype=torch.uint8, device="cuda")
+    mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])
+    with ec.Recovery(k, m, mat, 3, mask, 0, 7, p) as rec:
+        with pytest.raises(ec.CecError):  # D2 still missing after D1
+            rec.finish(1, np.zeros(8 * 4096, np.uint8), {}, {0: np.zeros(8 * 4096, np.uint8)})
