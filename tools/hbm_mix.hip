@@ -1,7 +1,11 @@
 // tools/hbm_mix.hip -- HBM ceiling per read:write mix on this MI355X (not product).
 // Each kernel streams R read arenas and W write arenas of `len` bytes with the access
-// shape of combine_kernel (one 4 KiB tile per 256-lane workgroup, 16 B per lane, nt
-// loads/stores), XOR-combining reads into every write; grid = tiles.  The GB/s of
+// shape of combine_kernel (a 4 KiB tile per 256 >> s lanes x 2^s workgroups, 16 B per
+// lane, nt loads/stores), XOR-combining reads into every write; grid = tiles << s.
+//   argv[1]: arena layout: 0 = separate hipMalloc per arena; "arena" = one allocation at
+//            the library's odd-4 KiB stride (cec_arena_stride); N = 2 MiB + i*N skew
+//   argv[2]: "const" = constant bytes instead of random
+//   argv[3]: lanes per workgroup (256, 128 or 64; default 256)  The GB/s of
 // each mix is the practical roofline for the op with that mix:
 //   encode RS(3,2) 3:2, decode single 3:1, RS(4,2) encode 4:2, drain 2:1 (RMW).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbm_mix.hip -o tools/hbm_mix.bin
@@ -31,7 +35,7 @@ struct Ptrs {
 
 template <int R, int W>
 __global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
-    const uint64_t off = (uint64_t)blockIdx.x * 4096 + threadIdx.x * 16;
+    const uint64_t off = (uint64_t)blockIdx.x * blockDim.x * 16 + threadIdx.x * 16;
     u32x4 acc = {0, 0, 0, 0};
 #pragma unroll
     for (int i = 0; i < R; ++i)
@@ -62,7 +66,13 @@ int main(int argc, char **argv) {
     const uint64_t len = 256ull << 20;  // per arena
     // argv[1] = skew in bytes: arena i starts i * skew past a 2 MiB boundary inside one
     // allocation (0 = separate hipMalloc per arena, the default layout)
-    const uint64_t skew = argc > 1 ? strtoull(argv[1], nullptr, 0) : 0;
+    const bool arena = argc > 1 && argv[1][0] == 'a';
+    const uint64_t skew = argc > 1 && !arena ? strtoull(argv[1], nullptr, 0) : 0;
+    const uint32_t lanes = argc > 3 ? (uint32_t)atoi(argv[3]) : 256;
+    if (lanes != 256 && lanes != 128 && lanes != 64) {
+        fprintf(stderr, "lanes must be 256, 128 or 64\n");
+        return 1;
+    }
     // argv[2] == "const": constant bytes (hipMemset) instead of random ones
     const bool constant = argc > 2 && argv[2][0] == 'c';
     auto fill = [&](uint8_t *b, int i) {
@@ -73,7 +83,18 @@ int main(int argc, char **argv) {
     printf("fill: %s\n", constant ? "constant" : "random");
     Ptrs p;
     std::vector<uint8_t *> bufs;
-    if (skew == 0) {
+    if (arena) {  // cec_arena_stride: an odd number of 4 KiB pages between bases
+        uint64_t pages = (len + 4095) / 4096;
+        if (pages % 2 == 0) ++pages;
+        const uint64_t stride = pages * 4096;
+        uint8_t *big;
+        CK(hipMalloc(&big, 10 * stride));
+        for (int i = 0; i < 10; ++i) {
+            uint8_t *b = big + i * stride;
+            fill(b, i);
+            bufs.push_back(b);
+        }
+    } else if (skew == 0) {
         for (int i = 0; i < 10; ++i) {
             uint8_t *b;
             CK(hipMalloc(&b, len));
@@ -90,7 +111,8 @@ int main(int argc, char **argv) {
             bufs.push_back(b);
         }
     }
-    printf("arena skew: %llu bytes\n", (unsigned long long)skew);
+    printf("arena layout: %s, %u lanes per workgroup\n",
+           arena ? "one allocation, odd-4KiB stride" : (skew ? "skewed" : "separate hipMalloc"), lanes);
     for (int i = 0; i < 6; ++i) p.r[i] = bufs[i];
     for (int j = 0; j < 4; ++j) p.w[j] = bufs[6 + j];
     uint32_t *sink;
@@ -103,19 +125,19 @@ int main(int argc, char **argv) {
                          {"1:1 copy", 1, 1}, {"2:1 (RMW-like)", 2, 1}, {"3:1 decode RS(3,2)", 3, 1},
                          {"3:2 encode RS(3,2)", 3, 2}, {"4:1 decode RS(4,2)", 4, 1},
                          {"4:2 encode RS(4,2)", 4, 2}, {"6:4 RS(6,4)-like", 6, 4}};
-    const uint32_t grid = len / 4096;
+    const uint32_t grid = len / (16 * lanes);
     auto launch = [&](const V &v) {
         switch (v.r * 10 + v.w) {
-        case 10: hipLaunchKernelGGL((k_mix<1, 0>), grid, 256, 0, 0, p, sink); break;
-        case 30: hipLaunchKernelGGL((k_mix<3, 0>), grid, 256, 0, 0, p, sink); break;
-        case 1: hipLaunchKernelGGL((k_mix<0, 1>), grid, 256, 0, 0, p, sink); break;
-        case 11: hipLaunchKernelGGL((k_mix<1, 1>), grid, 256, 0, 0, p, sink); break;
-        case 21: hipLaunchKernelGGL((k_mix<2, 1>), grid, 256, 0, 0, p, sink); break;
-        case 31: hipLaunchKernelGGL((k_mix<3, 1>), grid, 256, 0, 0, p, sink); break;
-        case 32: hipLaunchKernelGGL((k_mix<3, 2>), grid, 256, 0, 0, p, sink); break;
-        case 41: hipLaunchKernelGGL((k_mix<4, 1>), grid, 256, 0, 0, p, sink); break;
-        case 42: hipLaunchKernelGGL((k_mix<4, 2>), grid, 256, 0, 0, p, sink); break;
-        case 64: hipLaunchKernelGGL((k_mix<6, 4>), grid, 256, 0, 0, p, sink); break;
+        case 10: hipLaunchKernelGGL((k_mix<1, 0>), grid, lanes, 0, 0, p, sink); break;
+        case 30: hipLaunchKernelGGL((k_mix<3, 0>), grid, lanes, 0, 0, p, sink); break;
+        case 1: hipLaunchKernelGGL((k_mix<0, 1>), grid, lanes, 0, 0, p, sink); break;
+        case 11: hipLaunchKernelGGL((k_mix<1, 1>), grid, lanes, 0, 0, p, sink); break;
+        case 21: hipLaunchKernelGGL((k_mix<2, 1>), grid, lanes, 0, 0, p, sink); break;
+        case 31: hipLaunchKernelGGL((k_mix<3, 1>), grid, lanes, 0, 0, p, sink); break;
+        case 32: hipLaunchKernelGGL((k_mix<3, 2>), grid, lanes, 0, 0, p, sink); break;
+        case 41: hipLaunchKernelGGL((k_mix<4, 1>), grid, lanes, 0, 0, p, sink); break;
+        case 42: hipLaunchKernelGGL((k_mix<4, 2>), grid, lanes, 0, 0, p, sink); break;
+        case 64: hipLaunchKernelGGL((k_mix<6, 4>), grid, lanes, 0, 0, p, sink); break;
         }
     };
     hipEvent_t e0, e1;
@@ -134,8 +156,8 @@ int main(int argc, char **argv) {
             CK(hipEventElapsedTime(&t, e0, e1));
             ms[i].push_back(t / iters);
         }
-    printf("HBM ceilings by read:write mix, %llu MiB per arena, 4 KiB tile per workgroup, nt\n",
-           (unsigned long long)(len >> 20));
+    printf("HBM ceilings by read:write mix, %llu MiB per arena, %u B per workgroup, nt\n",
+           (unsigned long long)(len >> 20), lanes * 16);
     for (size_t i = 0; i < vs.size(); ++i) {
         std::sort(ms[i].begin(), ms[i].end());
         const double bytes = (double)(vs[i].r + vs[i].w) * len;

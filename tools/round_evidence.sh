@@ -1,6 +1,7 @@
 #!/bin/bash
 # tools/round_evidence.sh ROUND -- every measurement DESIGN.md quotes, on one box, one call
-# (run ON the GPU box through gpurun).  Results land in gpurun_out/evidence_ROUND/;
+# (run ON the GPU box through gpurun; build first, here: python -c 'import __graft_entry__ as g;
+# g.build()' && make -C tools).  Results land in gpurun_out/evidence_ROUND/;
 # copy what is quoted into profiles/r01_evidence/ here (cp gpurun_out/evidence_ROUND/{*.jsonl,hbm_mix.txt}),
 # and run tools/pmc_summary.py on the merged gpurun_out/prof_ROUND.
 set -euo pipefail
@@ -18,7 +19,10 @@ $B --no-cpu-baseline --workload rs32_1m    > "$OUT/bench_1m.jsonl"    2> "$OUT/b
 $B --e2e                               > "$OUT/bench_e2e.jsonl"     2> "$OUT/bench_e2e.err"
 $B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/bench_drain.err"
 $B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"
-timeout -k 10 200 tools/hbm_mix.bin    > "$OUT/hbm_mix.txt" 2>&1
+$B --ops                               > "$OUT/bench_ops.jsonl"     2> "$OUT/bench_ops.err"
+$B --ops --engine lds                  > "$OUT/bench_ops_lds.jsonl" 2> "$OUT/bench_ops_lds.err"
+timeout -k 10 200 tools/hbm_mix.bin arena random 64  > "$OUT/hbm_mix.txt" 2>&1
+timeout -k 10 200 tools/hbm_mix.bin arena random 256 >> "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
 [ -n "${EVID_NO_PROF:-}" ] || bash tools/profile_round.sh "$ROUND" > "$OUT/profile.log" 2>&1
 echo done > "$OUT/DONE"
