@@ -829,6 +829,61 @@ CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *conn
     return remaining ? 0u : mask;
 }
 
+// ============================================================== fast stream wait
+// One lane stores v into mapped pinned memory once every earlier op on the stream has
+// finished (stream order).
+__global__ void cec_signal_kernel(uint32_t *flag, uint32_t v) {
+    __threadfence_system();
+    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+namespace {
+struct SignalCtx {  // per thread and device: a mapped pinned completion word
+    int device = -1;
+    uint32_t *flag = nullptr, *flag_dev = nullptr;
+    uint32_t seq = 0;
+    ~SignalCtx() {
+        if (flag) (void)hipHostFree(flag);
+    }
+};
+thread_local SignalCtx t_signal;
+}  // namespace
+
+// Wait for everything enqueued on stream s, for the synchronous calls whose cost is
+// their latency (the per-call drop-in, per-SET recovery folds).  A one-lane kernel
+// writes a sequence number into mapped pinned memory behind the work and the host
+// spins on it: 6.3 us per empty call against 10.5 us for hipStreamSynchronize
+// (tools/launch_latency.hip, profiles/r01_launch_latency.txt).  After 200 us (a large
+// op, or a kernel that faulted and never signals) it falls back to
+// hipStreamSynchronize, which also reports errors.
+static int stream_wait(hipStream_t s) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    SignalCtx &c = t_signal;
+    if (c.device != dev) {
+        if (c.flag) HIP_TRY(hipHostFree(c.flag));
+        c.flag = c.flag_dev = nullptr;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.flag), 64,
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.flag_dev), c.flag, 0));
+        __atomic_store_n(c.flag, 0u, __ATOMIC_RELEASE);
+        c.seq = 0;
+        c.device = dev;
+    }
+    const uint32_t v = ++c.seq;
+    hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
+    HIP_TRY(hipGetLastError());
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; ++i) {
+        if (__atomic_load_n(c.flag, __ATOMIC_ACQUIRE) == v) return CEC_OK;
+        __builtin_ia32_pause();
+        if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200))
+            break;
+    }
+    HIP_TRY(hipStreamSynchronize(s));
+    return CEC_OK;
+}
+
 #include "cec_drain.inc"
 #include "cec_recovery.inc"
 
@@ -944,13 +999,6 @@ CEC_API int *jerasure_matrix_multiply(int *m1, int *m2, int r1, int c1, int r2, 
     return p;
 }
 
-// One lane stores v into mapped pinned memory once every earlier op on the stream has
-// finished (stream order): the drop-in's completion signal.
-__global__ void cec_signal_kernel(uint32_t *flag, uint32_t v) {
-    __threadfence_system();
-    __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // Per-thread context of the synchronous drop-in: a stream and device staging.
 namespace {
 struct DropInCtx {
@@ -961,9 +1009,6 @@ struct DropInCtx {
     uint8_t *zc = nullptr;  // mapped pinned buffer (2 x zc_cap) for zero-copy calls
     void *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
-    uint32_t *flag = nullptr;  // mapped pinned completion word (cec_signal_kernel)
-    uint32_t *flag_dev = nullptr;
-    uint32_t seq = 0;
     ~DropInCtx() {
         if (stream) {
             (void)hipStreamSynchronize(stream);
@@ -972,7 +1017,6 @@ struct DropInCtx {
         if (dsrc) (void)hipFree(dsrc);
         if (ddst) (void)hipFree(ddst);
         if (zc) (void)hipHostFree(zc);
-        if (flag) (void)hipHostFree(flag);
     }
 };
 thread_local DropInCtx t_ctx;
@@ -1023,33 +1067,6 @@ void *device_view(void *p) {
         }                                                                                   \
     } while (0)
 
-// Wait for everything enqueued on the drop-in stream.  A one-lane kernel writes a
-// sequence number into mapped pinned memory after the op and the host spins on it:
-// 6.3 us per empty call against 10.5 us for hipStreamSynchronize
-// (tools/launch_latency.hip, profiles/r01_launch_latency.txt).  After 200 us (a large
-// call, or a kernel that faulted and never signals) it falls back to
-// hipStreamSynchronize, which also reports errors.
-static void dropin_wait(DropInCtx &c) {
-    if (!c.flag) {
-        DROPIN_HIP(hipHostMalloc(reinterpret_cast<void **>(&c.flag), 64,
-                                 hipHostMallocMapped | hipHostMallocCoherent));
-        DROPIN_HIP(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.flag_dev), c.flag, 0));
-        __atomic_store_n(c.flag, 0u, __ATOMIC_RELEASE);
-    }
-    const uint32_t v = ++c.seq;
-    hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, c.stream, c.flag_dev, v);
-    DROPIN_HIP(hipGetLastError());
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t i = 1;; ++i) {
-        if (__atomic_load_n(c.flag, __ATOMIC_ACQUIRE) == v) return;
-        __builtin_ia32_pause();
-        if ((i & 1023) == 0 &&
-            std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200))
-            break;
-    }
-    DROPIN_HIP(hipStreamSynchronize(c.stream));
-}
-
 CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, char *r2, int add) {
     if (multby < 0 || multby > 255) die("galois_w08_region_multiply: multby outside [0, 255]");
     if (nbytes <= 0) return;
@@ -1066,11 +1083,9 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         c.dsrc = c.ddst = nullptr;
         c.cap = 0;
         if (c.zc) DROPIN_HIP(hipHostFree(c.zc));  // device addresses are per device
-        if (c.flag) DROPIN_HIP(hipHostFree(c.flag));
         c.zc = nullptr;
         c.zc_dev = nullptr;
         c.zc_cap = 0;
-        c.flag = c.flag_dev = nullptr;
         DROPIN_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
         c.device = dev;
     }
@@ -1080,7 +1095,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     void *vs = device_view(region), *vd = device_view(dst);
     if (vs && vd) {  // device-resident (or pinned/mapped): run in place
         DROPIN_CHECK(cec_region_multiply(vs, multby, n, vd, mode_add, c.stream));
-        dropin_wait(c);
+        DROPIN_CHECK(stream_wait(c.stream));
         return;
     }
     if (n <= zero_copy_max()) {  // small pageable call: zero-copy through mapped pinned memory
@@ -1096,7 +1111,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         if (mode_add) memcpy(zd, dst, n);
         uint8_t *ds = static_cast<uint8_t *>(c.zc_dev), *dd = ds + c.zc_cap;
         DROPIN_CHECK(cec_region_multiply(ds, multby, n, dd, mode_add, c.stream));
-        dropin_wait(c);  // (spinning on hipStreamQuery instead: no gain)
+        DROPIN_CHECK(stream_wait(c.stream));  // (spinning on hipStreamQuery instead: no gain)
         memcpy(dst, zd, n);
         return;
     }
