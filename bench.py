@@ -60,7 +60,7 @@ def parse(argv=None):
                     help="device-resident roofline of every SURVEY §8a op (a1-a7 + fused decode)")
     ap.add_argument("--e2e-chunk", type=int, default=4096, help="stripes per pipelined chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU work budget (thread-seconds)")
+    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="CPU work budget (thread-seconds)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for the barrier / max-over-ranks (nccl = RCCL)")
     return ap.parse_args(argv)
@@ -108,7 +108,8 @@ def cpu_baseline(k, m, n, budget_s):
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = max(1, min(threads, 16))
     stripes = max(threads, (64 << 20) // n)  # 64 MiB per shard: larger than the host LLC
-    t1 = pyoracle.bench_encode_decode(k, m, n, stripes, threads, 1, True)
+    pyoracle.bench_encode_decode(k, m, n, stripes, threads, 1, True)  # first touch
+    t1 = pyoracle.bench_encode_decode(k, m, n, stripes, threads, 4, True) / 4  # calibrate
     reps = max(1, min(2000, int(budget_s / max(t1 * threads, 1e-6))))
     t = pyoracle.bench_encode_decode(k, m, n, stripes, threads, reps, True)
     payload = (k + 1) * n * stripes * reps
