@@ -127,3 +127,22 @@ def test_bad_arguments_rejected(lib):
     assert ei.value.code == lib.CEC_EINVAL
     assert lib.recovery_mask(3, 2, 3, [1, 1, 1, 1, 1]) == 0b01011
     assert lib.recovery_mask(3, 2, 3, [0, 0, 1, 1, 0]) == 0
+
+
+@pytest.mark.parametrize("k,m", [(3, 2), (4, 2), (6, 3)])
+def test_recovery_mask_matches_oracle_every_pattern(lib, oracle, k, m):
+    """cec_recovery_mask == start_recovery's selection (memcached.c:8136-8151, via the
+    oracle) for every leader and every connectivity pattern; host logic, no GPU."""
+    import itertools
+
+    for leader in range(k + m):
+        for conn in itertools.product([0, 1], repeat=k + m):
+            conn = list(conn)
+            assert lib.recovery_mask(k, m, leader, conn) == oracle.recovery_mask(k, m, leader, conn)
+
+
+def test_arena_stride_is_odd_pages(lib):
+    """cec_arena_stride: an odd number of 4 KiB pages covering the arena."""
+    for n in [1, 4095, 4096, 8192, 12288, (256 << 20), (256 << 20) + 1, 3 * 4096 + 5]:
+        s = lib.arena_stride(n)
+        assert s >= n and s % 4096 == 0 and (s // 4096) % 2 == 1 and s - n < 2 * 4096
