@@ -262,16 +262,10 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
         const int n_in = kExact ? NT : P->n_in;
         const int n_out = kExact ? LT : P->n_out;
         if (!kExact && n_out == 0) continue;
-        if constexpr (Eng::kStaged) {
-            // Stage this pattern's rows (L2-resident, 256 B each; 512 B for an RS(3,2)
-            // encode).  The barrier before re-staging only matters when a workgroup
-            // walks several tiles (more than 2^31 work items).
+        // A workgroup that walks several tiles (more than 2^31 work items) must not
+        // re-stage LDS rows while lanes still read the previous tile's.
+        if constexpr (Eng::kStaged)
             if (g != blockIdx.x) __syncthreads();
-            const uint32_t nb = static_cast<uint32_t>(P->lds_rows) * 256u;
-            const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
-            for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
-            __syncthreads();
-        }
         auto is_acc = [&](int l) -> bool {
             if constexpr (kAcc == kAccNone) return false;
             else if constexpr (kAcc == kAccAll) return true;
@@ -303,12 +297,15 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
         // rarely a multiple of 16) and tiles of misaligned device pointers use the
         // branch-free byte gather / scatter, everything else dwordx4.
         const uint32_t pos = lane * 16;
-        if (pos >= tr.len) continue;
-        const uint32_t cnt = min(16u, tr.len - pos);
+        const bool active = pos < tr.len;
+        if constexpr (!Eng::kStaged)
+            if (!active) continue;  // (staged engines keep every lane to the barrier)
+        const uint32_t cnt = active ? min(16u, tr.len - pos) : 16u;
         const bool wide = (mis & 15) == 0 && cnt == 16;
         uint4 x[NT];
         uint4 acc[LT];
-        if (wide) {
+        if (!active) {
+        } else if (wide) {
 #pragma unroll
             for (int i = 0; i < NT; ++i)
                 if (i < n_in) x[i] = ld16(in[i], pos);
@@ -326,6 +323,15 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
                 acc[l] = make_uint4(0, 0, 0, 0);
                 if (l < n_out && is_acc(l)) acc[l] = gather16(out[l], pos, cnt);
             }
+        }
+        if constexpr (Eng::kStaged) {
+            // Stage this pattern's product rows (L2-resident, 256 B each; 512 B for an
+            // RS(3,2) encode) while the stream loads above are in flight.
+            const uint32_t nb = static_cast<uint32_t>(P->lds_rows) * 256u;
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
+            for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
+            __syncthreads();
+            if (!active) continue;
         }
         compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
         if (wide) {

@@ -63,10 +63,11 @@ typedef struct cec_extent {
  * walk (load balance across mixed 256 B .. 1 MiB values).  Build once per batch. */
 typedef struct cec_plan cec_plan;
 
-/* GF(2^8) engine used by the kernels.  Both are bit-exact; PERM (default) looks up
- * three 8-entry byte tables per coefficient with v_perm_b32 (pure VALU); LDS stages
- * one 256-entry product row per coefficient, exp[log x + log c] built from the
- * log / antilog tables, in LDS (one ds_read_u8 per byte). */
+/* GF(2^8) engine used by the kernels.  Both are bit-exact and within 1-2 % of each
+ * other.  PERM (default) looks up three 8-entry byte tables per coefficient with
+ * v_perm_b32 (pure VALU, no LDS); LDS stages one 256-entry product row per
+ * coefficient, exp[log x + log c] built from the log / antilog tables, in LDS (one
+ * ds_read_u8 per byte). */
 typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1 } cec_engine;
 
 /* ---- runtime ---- */

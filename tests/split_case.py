@@ -21,9 +21,17 @@ def main() -> None:
     torch.cuda.set_device(0)
     torch.empty(1, device="cuda")
     from cocytus_amd import ec
-    from oracle import pyoracle
 
     assert ec.device_check() == ec.CEC_OK, ec.lib().cec_last_error()
+    for engine in (ec.CEC_ENGINE_LDS, ec.CEC_ENGINE_PERM):  # both GF engines per split
+        ec.set_engine(engine)
+        check(torch, ec)
+    print("OK")
+
+
+def check(torch, ec) -> None:
+    from oracle import pyoracle
+
     k, m = 3, 2
     mat = ec.coding_matrix(k, m)
     rng = np.random.default_rng(int(os.environ.get("CEC_SPLIT_SHIFT", "9")) + 17)
@@ -90,7 +98,6 @@ def main() -> None:
         want = dst.copy()
         pyoracle.region_multiply(src[shift:shift + n].copy(), 0x53, want[shift:shift + n], 1)
         assert np.array_equal(dd.cpu().numpy(), want), f"region shift {shift}"
-    print("OK")
 
 
 if __name__ == "__main__":

@@ -146,3 +146,10 @@ def test_arena_stride_is_odd_pages(lib):
     for n in [1, 4095, 4096, 8192, 12288, (256 << 20), (256 << 20) + 1, 3 * 4096 + 5]:
         s = lib.arena_stride(n)
         assert s >= n and s % 4096 == 0 and (s // 4096) % 2 == 1 and s - n < 2 * 4096
+
+
+def test_default_engine_is_perm(lib):
+    """The product default is the PERM engine (1-2 % ahead of the LDS engine in bench
+    processes); LDS stays selectable and both are in every GPU parity
+    test."""
+    assert lib.get_engine() == lib.CEC_ENGINE_PERM

@@ -24,9 +24,10 @@ SENT = 0xA5
 @pytest.fixture(params=["perm", "lds"])
 def engine(request, gpu):
     torch, ec = gpu
+    default = ec.get_engine()
     ec.set_engine(ec.CEC_ENGINE_PERM if request.param == "perm" else ec.CEC_ENGINE_LDS)
     yield request.param
-    ec.set_engine(ec.CEC_ENGINE_PERM)
+    ec.set_engine(default)
 
 
 def to_dev(torch, a: np.ndarray):
@@ -727,6 +728,7 @@ def test_fuzz_random_plans(gpu, oracle, seed):
     rng = np.random.default_rng(0xF022 + seed)
     k = int(rng.integers(2, 9))
     m = int(rng.integers(1, 5))
+    default = ec.get_engine()
     ec.set_engine(ec.CEC_ENGINE_LDS if seed % 2 else ec.CEC_ENGINE_PERM)
     try:
         mat = ec.coding_matrix(k, m)
@@ -796,7 +798,7 @@ def test_fuzz_random_plans(gpu, oracle, seed):
         for j in range(k):
             assert np.array_equal(to_host(odev[j]), out[j]), ("decode", j)
     finally:
-        ec.set_engine(ec.CEC_ENGINE_PERM)
+        ec.set_engine(default)
 
 
 # ------------------------------------------------------------------ reference allocator layout
