@@ -886,6 +886,7 @@ static int stream_wait(hipStream_t s) {
 
 #include "cec_drain.inc"
 #include "cec_recovery.inc"
+#include "cec_pool.inc"
 
 // ============================================================== events / streams
 CEC_API int cec_event_create(void **ev) {

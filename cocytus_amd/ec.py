@@ -25,6 +25,7 @@ CEC_EHIP = -3
 CEC_ENOMEM = -4
 CEC_EOVERLAP = -5
 CEC_ENODEV = -6
+CEC_EFULL = -7
 CEC_ENGINE_PERM = 0
 CEC_ENGINE_LDS = 1
 CEC_MAX_K = 16
@@ -113,6 +114,17 @@ _SIGS = {
     "cec_recovery_bytes": ([_vp], ctypes.c_uint64),
     "cec_recovery_solve": ([_vp, _pp, _pp, _vp], _i),
     "cec_recovery_finish": ([_vp, _i, _vp, _pp, _pp, _vp], _i),
+    "cec_recovery_pool_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, _vp, _i], _i),
+    "cec_recovery_pool_destroy": ([_vp], _i),
+    "cec_recovery_pool_begin": ([_vp, _u32, _i, _i], _i),
+    "cec_recovery_pool_add_peer": ([_vp, _i, _i, _vp], _i),
+    "cec_recovery_pool_flush": ([_vp, _vp], _i),
+    "cec_recovery_pool_complete": ([_vp, _i], _i),
+    "cec_recovery_pool_fold_update": ([_vp, _i, ctypes.c_uint64, _vp, _u32, _vp], _i),
+    "cec_recovery_pool_solve": ([_vp, _ip, _i, _pp, _vp], _i),
+    "cec_recovery_pool_residual": ([_vp, _i, _vp, _vp], _i),
+    "cec_recovery_pool_end": ([_vp, _i], _i),
+    "cec_recovery_pool_active": ([_vp], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
     "cec_event_destroy": ([_vp], _i),
     "cec_event_record": ([_vp, _vp], _i),
@@ -456,6 +468,77 @@ class Recovery:
         try:
             if self._h and _lib is not None:
                 _lib.cec_recovery_destroy(self._h)
+        except Exception:
+            pass
+
+
+class RecoveryPool:
+    """cec_recovery_pool: many small in-flight recovery requests of one parity, their
+    replies folded in one launch per flush (the idle recoverer, §8f rank 2)."""
+
+    def __init__(self, k, m, matrix, lid_self, parity_arena, capacity_units=1024):
+        self.k, self.m = k, m
+        self._h = ctypes.c_void_p()
+        _check(lib().cec_recovery_pool_create(ctypes.byref(self._h), k, m, _int_array(matrix), lid_self,
+                                              _ptr(parity_arena), capacity_units))
+
+    def begin(self, mask: int, unit_begin: int, unit_end: int) -> int:
+        rc = lib().cec_recovery_pool_begin(self._h, mask, unit_begin, unit_end)
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    def add_peer(self, rid: int, peer_lid: int, units) -> None:
+        _check(lib().cec_recovery_pool_add_peer(self._h, rid, peer_lid, _host_or_dev(units)))
+
+    def flush(self, stream=None) -> int:
+        rc = lib().cec_recovery_pool_flush(self._h, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    def complete(self, rid: int) -> bool:
+        return bool(lib().cec_recovery_pool_complete(self._h, rid))
+
+    def fold_update(self, peer_lid: int, addr: int, diff, stream=None) -> int:
+        n = diff.nbytes if hasattr(diff, "nbytes") else len(diff)
+        rc = lib().cec_recovery_pool_fold_update(self._h, peer_lid, addr, _host_or_dev(diff), n, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    def solve(self, rids, out_arenas, stream=None) -> None:
+        """out_arenas: k device arenas by data lid (None where not lost)."""
+        ids = (ctypes.c_int * len(rids))(*rids)
+        oo = (ctypes.c_void_p * self.k)(*[_ptr(out_arenas[j]) if j < len(out_arenas) and
+                                          out_arenas[j] is not None else None for j in range(self.k)])
+        _check(lib().cec_recovery_pool_solve(self._h, ids, len(rids), oo, _stream(stream)))
+
+    def residual(self, rid: int, dst, stream=None) -> None:
+        _check(lib().cec_recovery_pool_residual(self._h, rid, _host_or_dev(dst), _stream(stream)))
+
+    def end(self, rid: int) -> None:
+        _check(lib().cec_recovery_pool_end(self._h, rid))
+
+    @property
+    def active(self) -> int:
+        return int(lib().cec_recovery_pool_active(self._h))
+
+    def destroy(self) -> None:
+        if self._h:
+            _check(lib().cec_recovery_pool_destroy(self._h))
+            self._h = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.destroy()
+
+    def __del__(self):
+        try:
+            if self._h and _lib is not None:
+                _lib.cec_recovery_pool_destroy(self._h)
         except Exception:
             pass
 

@@ -43,7 +43,8 @@ typedef enum cec_status {
     CEC_EHIP = -3,        /* a HIP runtime call failed; see cec_last_error() */
     CEC_ENOMEM = -4,      /* device or pinned-host allocation failed */
     CEC_EOVERLAP = -5,    /* read-modify-write op on a plan whose extents overlap */
-    CEC_ENODEV = -6       /* no usable gfx950 device: there is no CPU fallback */
+    CEC_ENODEV = -6,      /* no usable gfx950 device: there is no CPU fallback */
+    CEC_EFULL = -7        /* a recovery pool has no room for the request */
 } cec_status;
 
 /* One value of a batch.  `off` addresses the arenas (item->addr, memcached.h:441);
@@ -247,6 +248,43 @@ int cec_recovery_solve(cec_recovery *leader, const void *const *peer_residuals,
  * buffers take the two-step path.  EINVAL if peer is not the last data peer. */
 int cec_recovery_finish(cec_recovery *leader, int peer_lid, const void *units,
                         const void *const *peer_residuals, void *const *out, void *stream);
+
+/* ---- background recovery of many small unit ranges ----
+ * The idle recoverer issues one 4 KiB unit per request, up to TOO_MANY_RECOVERY = 85
+ * in flight (idle_event_handler, memcached.c:5712-5734; const.h:27).  A pool keeps
+ * every in-flight request's residual in one HBM buffer: replies are queued with a
+ * host memcpy into per-peer pinned staging, and cec_recovery_pool_flush folds all of
+ * them in ONE launch (first-touch parity copy fused, recovery.c:61-96).  The leader
+ * solves any number of complete single-loss requests in one launch into the lost
+ * lids' arenas (memcached.c:7842-7922).  Same bytes as the reference chain. */
+typedef struct cec_recovery_pool cec_recovery_pool;
+
+int cec_recovery_pool_create(cec_recovery_pool **out, int k, int m, const int *matrix, int lid_self,
+                             const uint8_t *parity_arena /* device */, int capacity_units);
+int cec_recovery_pool_destroy(cec_recovery_pool *pool);
+/* start_recovery / do_recovery: returns the request id (>= 0), CEC_EFULL when the pool
+ * has no unit_end - unit_begin + 1 free contiguous units, or CEC_EINVAL. */
+int cec_recovery_pool_begin(cec_recovery_pool *pool, uint32_t mask, int unit_begin, int unit_end);
+/* complete_recovery_nread: data peer peer_lid's raw units of request id (host or
+ * device).  Queued, not yet folded. */
+int cec_recovery_pool_add_peer(cec_recovery_pool *pool, int id, int peer_lid, const void *units);
+/* Fold every queued reply in one launch; returns the requests folded (>= 0). */
+int cec_recovery_pool_flush(cec_recovery_pool *pool, void *stream);
+/* check_recovery_1st_completeness: every data lid of the request's mask applied or queued. */
+int cec_recovery_pool_complete(const cec_recovery_pool *pool, int id);
+/* recovery_try_update_unit for every request of the pool (flushes first); returns the
+ * units folded (>= 0) or a negative cec_status. */
+int cec_recovery_pool_fold_update(cec_recovery_pool *pool, int peer_lid, uint64_t addr, const void *diff,
+                                  uint32_t len, void *stream);
+/* Leader, single loss: out[lost lid] (k device arenas by data lid, arena-addressed) =
+ * inv * residual for every listed complete request, one launch (flushes first). */
+int cec_recovery_pool_solve(cec_recovery_pool *pool, const int *ids, int n, uint8_t *const *out,
+                            void *stream);
+/* Non-leader: copy request id's residual (its units x 4 KiB) to dst (host or device). */
+int cec_recovery_pool_residual(cec_recovery_pool *pool, int id, void *dst, void *stream);
+/* recovery_req_remove: release the request's units. */
+int cec_recovery_pool_end(cec_recovery_pool *pool, int id);
+int cec_recovery_pool_active(const cec_recovery_pool *pool);
 
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
 int cec_event_create(void **ev);

@@ -965,3 +965,102 @@ def test_recovery_finish_rejects_early_peer(gpu, oracle):
     with ec.Recovery(k, m, mat, 3, mask, 0, 7, p) as rec:
         with pytest.raises(ec.CecError):  # D2 still missing after D1
             rec.finish(1, np.zeros(8 * 4096, np.uint8), {}, {0: np.zeros(8 * 4096, np.uint8)})
+
+
+# ------------------------------------------------------------------ recovery pool (§8f 2)
+@pytest.mark.parametrize("engine_name", ["perm", "lds"])
+def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
+    """The idle recoverer's traffic (memcached.c:5712-5734): single-unit and short-range
+    requests, a bounded window in flight, replies from D1 / D2 in random order, flushes at
+    random points, SETs on D1 / D2 landing mid-recovery (fold_update, then the parity
+    apply, memcached.c:7757-7764), batched leader solves.  Every rebuilt unit of lost D0
+    equals the live data."""
+    torch, ec = gpu
+    default = ec.get_engine()
+    ec.set_engine(ec.CEC_ENGINE_PERM if engine_name == "perm" else ec.CEC_ENGINE_LDS)
+    try:
+        k, m, U = 3, 2, 4096
+        mat = ec.coding_matrix(k, m)
+        rng = np.random.default_rng(0x9001 + len(engine_name))
+        nunits = 256
+        data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+        p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
+        out0 = torch.zeros(nunits * U, dtype=torch.uint8, device="cuda")
+        mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])  # D0 lost, leader P0
+        pending, done = {}, []  # id -> (ub, ue, peers left)
+        next_unit, window = 0, 24
+        with ec.RecoveryPool(k, m, mat, 3, p0, capacity_units=64) as pool:
+            while next_unit < nunits or pending:
+                while next_unit < nunits and len(pending) < window:
+                    n = 1 if rng.random() < 0.7 else int(rng.integers(2, 5))
+                    ub, ue = next_unit, min(nunits - 1, next_unit + n - 1)
+                    try:
+                        pending[pool.begin(mask, ub, ue)] = (ub, ue, [1, 2])
+                    except ec.CecError as e:  # pool full: back off like the TOO_MANY check
+                        assert e.code == ec.CEC_EFULL
+                        break
+                    next_unit = ue + 1
+                rid = list(pending)[int(rng.integers(0, len(pending)))]
+                ub, ue, left = pending[rid]
+                peer = left.pop(int(rng.integers(0, len(left))))
+                pool.add_peer(rid, peer, data[peer][ub * U:(ue + 1) * U].copy())
+                if rng.random() < 0.3:
+                    pool.flush()
+                if rng.random() < 0.25:  # a SET on a surviving data shard lands
+                    j = int(rng.integers(1, 3))
+                    ln = int(rng.integers(1, 9000))
+                    addr = int(rng.integers(0, nunits * U - ln)) // 16 * 16
+                    new = rng.integers(0, 256, ln, dtype=np.uint8)
+                    diff = oracle.set_diff(data[j][addr:addr + ln].copy(), new)
+                    data[j][addr:addr + ln] = new
+                    pool.fold_update(j, addr, diff)
+                    ec.region_multiply(to_dev(torch, diff), mat[3 * k + j], ln, p0.data_ptr() + addr, 1)
+                    torch.cuda.synchronize()
+                if not left:
+                    assert pool.complete(rid)
+                    done.append(rid)
+                    del pending[rid]
+                if done and (rng.random() < 0.3 or not pending):
+                    pool.solve(done, [out0, None, None])
+                    for d in done:
+                        pool.end(d)
+                    done = []
+            assert pool.active == 0
+        torch.cuda.synchronize()
+        assert np.array_equal(to_host(out0), data[0])
+    finally:
+        ec.set_engine(default)
+
+
+def test_recovery_pool_non_leader_residual_and_errors(gpu, oracle):
+    """Double loss (D0, D1; mask {D2, P0, P1}): the non-leader P1's pooled residual equals
+    recovery_recover_units (recovery.c:61-96); the pool refuses a multi-loss solve, a
+    repeated peer, an incomplete solve and a request beyond its capacity."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    nunits = 32
+    data = [oracle.splitmix_bytes(0xC0C70200 + j, nunits * U) for j in range(k)]
+    parity = oracle.encode(mat, k, m, data)
+    p1 = to_dev(torch, parity[1])
+    with ec.RecoveryPool(k, m, mat, 4, p1, capacity_units=8) as pool:
+        rid = pool.begin(0b11100, 5, 7)
+        assert not pool.complete(rid)
+        with pytest.raises(ec.CecError):
+            pool.solve([rid], [torch.zeros(nunits * U, dtype=torch.uint8, device="cuda")] * 3)
+        pool.add_peer(rid, 2, data[2][5 * U:8 * U].copy())
+        with pytest.raises(ec.CecError):
+            pool.add_peer(rid, 2, data[2][5 * U:8 * U].copy())
+        assert pool.complete(rid)
+        res = np.zeros(3 * U, np.uint8)
+        pool.residual(rid, res)
+        exp = np.empty(3 * U, np.uint8)
+        oracle.recover_units(mat, k, 4, 2, parity[1][5 * U:8 * U].copy(), data[2][5 * U:8 * U].copy(), exp, [0])
+        assert np.array_equal(res, exp)
+        with pytest.raises(ec.CecError):  # two lost shards: the leader needs other residuals
+            pool.solve([rid], [torch.zeros(nunits * U, dtype=torch.uint8, device="cuda")] * 3)
+        with pytest.raises(ec.CecError) as ei:
+            pool.begin(0b11100, 10, 15)  # 6 more units, 5 free
+        assert ei.value.code == ec.CEC_EFULL
+        pool.end(rid)
+        assert pool.begin(0b11100, 10, 17) >= 0  # room again
