@@ -119,6 +119,9 @@ _SIGS = {
     "cec_recovery_pool_begin": ([_vp, _u32, _i, _i], _i),
     "cec_recovery_pool_add_peer": ([_vp, _i, _i, _vp], _i),
     "cec_recovery_pool_flush": ([_vp, _vp], _i),
+    "cec_recovery_pool_flush_solve": ([_vp, _pp, _vp], _i),
+    "cec_recovery_pool_solved": ([_vp, _i], _i),
+    "cec_recovery_pool_staging": ([_vp, _i, _i, ctypes.POINTER(ctypes.c_size_t)], _vp),
     "cec_recovery_pool_complete": ([_vp, _i], _i),
     "cec_recovery_pool_fold_update": ([_vp, _i, ctypes.c_uint64, _vp, _u32, _vp], _i),
     "cec_recovery_pool_solve": ([_vp, _ip, _i, _pp, _vp], _i),
@@ -489,13 +492,37 @@ class RecoveryPool:
         return rc
 
     def add_peer(self, rid: int, peer_lid: int, units) -> None:
-        _check(lib().cec_recovery_pool_add_peer(self._h, rid, peer_lid, _host_or_dev(units)))
+        """units: host / device buffer, or the address from staging() (no copy)."""
+        ptr = units if isinstance(units, int) else _host_or_dev(units)
+        _check(lib().cec_recovery_pool_add_peer(self._h, rid, peer_lid, ptr))
+
+    def staging(self, rid: int, peer_lid: int):
+        """(address, numpy uint8 view) where peer_lid's reply for rid may be received in place."""
+        import numpy as np
+
+        n = ctypes.c_size_t()
+        addr = lib().cec_recovery_pool_staging(self._h, rid, peer_lid, ctypes.byref(n))
+        if not addr:
+            _check(CEC_EINVAL)
+        return addr, np.ctypeslib.as_array((ctypes.c_uint8 * n.value).from_address(addr))
 
     def flush(self, stream=None) -> int:
         rc = lib().cec_recovery_pool_flush(self._h, _stream(stream))
         if rc < 0:
             _check(rc)
         return rc
+
+    def flush_solve(self, out_arenas, stream=None) -> int:
+        """flush(), also solving every single-loss request it completes into out_arenas."""
+        oo = (ctypes.c_void_p * self.k)(*[_ptr(out_arenas[j]) if j < len(out_arenas) and
+                                          out_arenas[j] is not None else None for j in range(self.k)])
+        rc = lib().cec_recovery_pool_flush_solve(self._h, oo, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    def solved(self, rid: int) -> bool:
+        return bool(lib().cec_recovery_pool_solved(self._h, rid))
 
     def complete(self, rid: int) -> bool:
         return bool(lib().cec_recovery_pool_complete(self._h, rid))

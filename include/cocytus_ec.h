@@ -268,8 +268,16 @@ int cec_recovery_pool_begin(cec_recovery_pool *pool, uint32_t mask, int unit_beg
 /* complete_recovery_nread: data peer peer_lid's raw units of request id (host or
  * device).  Queued, not yet folded. */
 int cec_recovery_pool_add_peer(cec_recovery_pool *pool, int id, int peer_lid, const void *units);
+/* Where peer peer_lid's reply for request id may be received in place (pinned, mapped;
+ * *len bytes): add_peer on this pointer copies nothing. */
+uint8_t *cec_recovery_pool_staging(cec_recovery_pool *pool, int id, int peer_lid, size_t *len);
 /* Fold every queued reply in one launch; returns the requests folded (>= 0). */
 int cec_recovery_pool_flush(cec_recovery_pool *pool, void *stream);
+/* The same launch also solves every request it completes that is a single loss led by
+ * this parity: out[lost lid] (k device arenas by data lid, arena-addressed) =
+ * inv * residual.  Returns the requests solved; cec_recovery_pool_solved tells which. */
+int cec_recovery_pool_flush_solve(cec_recovery_pool *pool, uint8_t *const *out, void *stream);
+int cec_recovery_pool_solved(const cec_recovery_pool *pool, int id);
 /* check_recovery_1st_completeness: every data lid of the request's mask applied or queued. */
 int cec_recovery_pool_complete(const cec_recovery_pool *pool, int id);
 /* recovery_try_update_unit for every request of the pool (flushes first); returns the

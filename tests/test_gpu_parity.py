@@ -1003,9 +1003,17 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
                 rid = list(pending)[int(rng.integers(0, len(pending)))]
                 ub, ue, left = pending[rid]
                 peer = left.pop(int(rng.integers(0, len(left))))
-                pool.add_peer(rid, peer, data[peer][ub * U:(ue + 1) * U].copy())
+                if rng.random() < 0.5:  # received straight into the pool's staging
+                    addr, view = pool.staging(rid, peer)
+                    view[:] = data[peer][ub * U:(ue + 1) * U]
+                    pool.add_peer(rid, peer, addr)
+                else:
+                    pool.add_peer(rid, peer, data[peer][ub * U:(ue + 1) * U].copy())
                 if rng.random() < 0.3:
-                    pool.flush()
+                    if rng.random() < 0.5:
+                        pool.flush()
+                    else:  # the completed single-loss requests are rebuilt in the same pass
+                        pool.flush_solve([out0, None, None])
                 if rng.random() < 0.25:  # a SET on a surviving data shard lands
                     j = int(rng.integers(1, 3))
                     ln = int(rng.integers(1, 9000))
@@ -1018,8 +1026,11 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
                     torch.cuda.synchronize()
                 if not left:
                     assert pool.complete(rid)
-                    done.append(rid)
                     del pending[rid]
+                    if pool.solved(rid):
+                        pool.end(rid)
+                    else:
+                        done.append(rid)
                 if done and (rng.random() < 0.3 or not pending):
                     pool.solve(done, [out0, None, None])
                     for d in done:
