@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/round_evidence.sh ROUND -- every measurement DESIGN.md quotes, on one box, one call
 # (run ON the GPU box through gpurun; build first, here: python -c 'import __graft_entry__ as g;
-# g.build()' && make -C tools).  Results land in gpurun_out/evidence_ROUND/;
+# g.build()' && make -C tools).  Copy the results into profiles/r01_evidence/.  Results land in gpurun_out/evidence_ROUND/;
 # copy what is quoted into profiles/r01_evidence/ here (cp gpurun_out/evidence_ROUND/{*.jsonl,hbm_mix.txt}),
 # and run tools/pmc_summary.py on the merged gpurun_out/prof_ROUND.
 set -euo pipefail
@@ -24,5 +24,7 @@ $B --ops --engine lds                  > "$OUT/bench_ops_lds.jsonl" 2> "$OUT/ben
 timeout -k 10 200 tools/hbm_mix.bin arena random 64  > "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/hbm_mix.bin arena random 256 >> "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
+timeout -k 10 200 tools/pool_bench.bin     > "$OUT/pool_bench.jsonl" 2>&1
+timeout -k 10 200 tools/launch_latency.bin > "$OUT/launch_latency.txt" 2>&1
 [ -n "${EVID_NO_PROF:-}" ] || bash tools/profile_round.sh "$ROUND" > "$OUT/profile.log" 2>&1
 echo done > "$OUT/DONE"
