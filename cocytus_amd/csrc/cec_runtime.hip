@@ -915,6 +915,13 @@ CEC_API int cec_stream_synchronize(void *stream) {
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return CEC_OK;
 }
+CEC_API int cec_copy(void *dst, const void *src, size_t n, void *stream) {
+    if (n && (!dst || !src)) return fail(CEC_EINVAL, "cec_copy: NULL pointer");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    if (n) HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
 
 // ============================================================== Jerasure drop-in
 CEC_API int galois_single_multiply(int a, int b, int w) {

@@ -300,6 +300,9 @@ int cec_event_destroy(void *ev);
 int cec_event_record(void *ev, void *stream);
 int cec_event_elapsed_ms(void *start, void *stop, float *ms); /* synchronises on stop */
 int cec_stream_synchronize(void *stream);
+/* Async copy between any host / device buffers (arena bytes to and from the server's
+ * buffers); complete after cec_stream_synchronize(stream). */
+int cec_copy(void *dst, const void *src, size_t n, void *stream);
 
 #ifdef __cplusplus
 }

@@ -77,3 +77,63 @@ def run_dropin_case(oracle, tmp_path, K=3, M=2, seed=0xC0C70001) -> None:
     assert got.size == exp.size
     assert np.array_equal(got, exp)
     assert np.array_equal(rec[0], data[1][lo:hi])  # the rebuilt shard is D1
+
+
+def run_batched_case(oracle, tmp_path, K=3, M=2, units=24, seed=0xC0C70B47) -> None:
+    """tests/dropin/batched_main.c (the batched bindings from C, no HIP header) vs the
+    reference's chains restated by the oracle: encode, per-SET diff-update with install,
+    the parity drain loop, and the idle recoverer's single-unit recoveries of D0."""
+    rng = np.random.default_rng(seed)
+    U = 4096
+    A = units * U
+    data = [rng.integers(0, 256, A, dtype=np.uint8) for _ in range(K)]
+    sets, vals, taken = [], [], [[] for _ in range(K)]
+    while len(sets) < 60:  # SETs never overlap within a shard; across shards they may
+        j = int(rng.integers(0, K))
+        n = int(rng.integers(1, 6000)) + 2
+        addr = int(rng.integers(0, (A - n) // 16)) * 16
+        if any(addr < e and s < addr + n for s, e in taken[j]):
+            continue
+        taken[j].append((addr, addr + n))
+        sets.append((j, addr, n))
+        vals.append(rng.integers(0, 256, n, dtype=np.uint8))
+    inp = tmp_path / "batched_in.bin"
+    with open(inp, "wb") as f:
+        f.write(np.array([K, M, units, len(sets)], np.int32).tobytes())
+        f.write(np.array(sets, np.int32).tobytes())
+        for d in data:
+            f.write(d.tobytes())
+        for v in vals:
+            f.write(v.tobytes())
+    exe = os.path.join(str(tmp_path), "batched_main")
+    subprocess.run(
+        ["gcc", "-O1", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+         os.path.join(HERE, "batched_main.c"), "-L", LIBDIR, "-lcocytus_ec",
+         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+        check=True,
+    )
+    outp = tmp_path / "batched_out.bin"
+    r = subprocess.run([exe, str(inp), str(outp)], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "OK", r.stderr + r.stdout
+    got = np.fromfile(outp, np.uint8).reshape(-1, A)
+
+    mat = oracle.big_vandermonde(K + M, K)
+    parity = oracle.encode(mat, K, M, data)
+    drained = parity[1].copy()
+    stale = [d.copy() for d in data]
+    for (j, addr, n), v in zip(sets, vals):  # the data side, SET by SET
+        old = data[j][addr:addr + n].copy()
+        pv = [p[addr:addr + n].copy() for p in parity]
+        oracle.diff_update(mat, K, M, j, old, v, pv, True)
+        data[j][addr:addr + n] = old
+        for p in range(M):
+            parity[p][addr:addr + n] = pv[p]
+    for (j, addr, n), v in zip(sets, vals):  # the parity's drain loop, one diff at a time
+        diff = oracle.set_diff(stale[j][addr:addr + n].copy(), v)
+        w = drained[addr:addr + n].copy()
+        oracle.parity_apply(mat, K, K + 1, j, diff, w)
+        drained[addr:addr + n] = w
+    exp = parity + data + [drained, data[0]]
+    assert got.shape[0] == len(exp)
+    for i, e in enumerate(exp):
+        assert np.array_equal(got[i], e), i

@@ -153,3 +153,14 @@ def test_default_engine_is_perm(lib):
     processes); LDS stays selectable and both are in every GPU parity
     test."""
     assert lib.get_engine() == lib.CEC_ENGINE_PERM
+
+
+def test_headers_are_c99_and_cxx(tmp_path):
+    """include/*.h compile as strict C99 (the reference server is C) and as C++."""
+    src = tmp_path / "h.c"
+    src.write_text("".join(f"#include <{h}>\n" for h in HEADERS) + "int main(void) { return 0; }\n")
+    inc = os.path.join(ROOT, "include")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", inc, "-c", str(src),
+                    "-o", str(tmp_path / "h.o")], check=True)
+    subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", inc, "-x", "c++", "-c", str(src),
+                    "-o", str(tmp_path / "hpp.o")], check=True)

@@ -1075,3 +1075,11 @@ def test_recovery_pool_non_leader_residual_and_errors(gpu, oracle):
         assert ei.value.code == ec.CEC_EFULL
         pool.end(rid)
         assert pool.begin(0b11100, 10, 17) >= 0  # room again
+
+
+def test_batched_bindings_c_program(gpu, oracle, tmp_path):
+    """The batched bindings from a C99 program (cec_encode_region, cec_diff_update,
+    cec_drainer_apply, cec_recovery_pool) vs the reference's chains."""
+    from tests.dropin import run_batched_case
+
+    run_batched_case(oracle, tmp_path)
