@@ -60,10 +60,17 @@ def parse(argv=None):
                     help="device-resident roofline of every SURVEY §8a op (a1-a7 + fused decode)")
     ap.add_argument("--e2e-chunk", type=int, default=4096, help="stripes per pipelined chunk")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--also", default="rs32_mixed,rs32_1m,rs42_64k",
+                    help="other workloads measured after the main one, reported under "
+                         "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=30.0, help="CPU work budget (thread-seconds)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for the barrier / max-over-ranks (nccl = RCCL)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    bad = [w for w in args.also.split(",") if w and w not in WORKLOADS]
+    if bad:
+        ap.error(f"--also: unknown workload(s) {bad}; choose from {sorted(WORKLOADS)}")
+    return args
 
 
 def layout(workload, seed=0xC0C70003):
@@ -165,11 +172,12 @@ def setup(backend="nccl"):
     return torch, dist, ec, world, rank
 
 
-def run_device(args):
-    torch, dist, ec, world, rank = setup(args.dist_backend)
-    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
-    k, m, n, _, what = WORKLOADS[args.workload]
-    stripes, arena = layout(args.workload)
+def measure_device(torch, dist, ec, world, rank, workload, args):
+    """Encode + rotating single-shard decode of `workload`, timed over args.steps.
+
+    Returns the rank-0 result fields (every rank returns them; only rank 0 prints)."""
+    k, m, n, _, what = WORKLOADS[workload]
+    stripes, arena = layout(workload)
     B = len(stripes)
     mat = ec.coding_matrix(k, m)
     g = torch.Generator(device="cuda").manual_seed(0xC0C70002 + rank)
@@ -194,18 +202,6 @@ def run_device(args):
         ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
     torch.cuda.synchronize()
 
-    import numpy as np
-
-    ok = True  # every rebuilt shard equals the original (compared on the device)
-    lost_of = [[x for x in range(k) if not (mk >> x) & 1][0] for mk in masks]
-    for j in range(k):
-        sel = np.zeros(arena, dtype=bool)
-        for s, (o, ln) in enumerate(stripes):
-            if lost_of[s % len(masks)] == j:
-                sel[o:o + ln] = True
-        sel_d = torch.from_numpy(sel).cuda()
-        ok &= bool(torch.equal(out[j][sel_d], data[j][sel_d]))
-
     evs = [[ec.Event() for _ in range(3)] for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -223,24 +219,83 @@ def run_device(args):
     elapsed = time.perf_counter() - t0
     enc_ms = sum(e[0].elapsed_ms(e[1]) for e in evs) / args.steps
     dec_ms = sum(e[1].elapsed_ms(e[2]) for e in evs) / args.steps
+    import numpy as np
+
+    ok = True  # every shard the timed steps rebuilt equals the original (on the device)
+    lost_of = [[x for x in range(k) if not (mk >> x) & 1][0] for mk in masks]
+    for j in range(k):
+        sel = np.zeros(arena, dtype=bool)
+        for s, (o, ln) in enumerate(stripes):
+            if lost_of[s % len(masks)] == j:
+                sel[o:o + ln] = True
+        sel_d = torch.from_numpy(sel).cuda()
+        ok &= bool(torch.equal(out[j][sel_d], data[j][sel_d]))
     elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist)
+    enc_plan.destroy()
+    dec_plan.destroy()
+    del arenas, data, parity, out
 
     payload = (k + 1) * bytes_total * world * args.steps
-    value = payload / elapsed / 2**30
     enc_bytes = (k + m) * bytes_total  # algorithmic HBM bytes per encode launch
     dec_bytes = (k + 1) * bytes_total  # per decode launch (read K survivors, write 1)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    enc_traffic, dec_traffic = load_traffic(args.workload)
+    enc_traffic, dec_traffic = load_traffic(workload)
+    return {
+        "k": k, "m": m, "n": n, "B": B, "what": what, "bytes_total": bytes_total,
+        "value": payload / elapsed / 2**30,
+        "ms_per_step": elapsed * 1e3 / args.steps,
+        "verified": ok and bad == 0.0,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(enc_gbps, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
+            "traffic": enc_traffic,
+            "kernel": f"combine_kernel<{k},{m},{'PermEngine' if args.engine == 'perm' else 'LdsEngine'},"
+                      "kAccNone,exact> (cec_encode)",
+            "algorithmic_bytes_per_launch": enc_bytes,
+            "launch_ms": round(enc_ms, 4),
+        },
+        "decode_roofline": {
+            "achieved": round(dec_gbps, 1), "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
+            "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(dec_ms, 4),
+            "traffic": dec_traffic,
+        },
+    }
+
+
+def run_device(args):
+    torch, dist, ec, world, rank = setup(args.dist_backend)
+    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+    r = measure_device(torch, dist, ec, world, rank, args.workload, args)
+    # The other device-resident BASELINE configs at the same N, on the same ranks, so the
+    # 1/2/4/8-GPU scaling run also covers configs[3] (RS(4,2) 64 KiB, an 8-GPU config)
+    # and the north star's 1 MiB values.  `value` stays the metric's workload.
+    also = {}
+    for w in [x for x in args.also.split(",") if x and x != args.workload]:
+        torch.cuda.empty_cache()
+        o = measure_device(torch, dist, ec, world, rank, w, args)
+        also[w] = {
+            "value": round(o["value"], 2), "unit": "GiB/s",
+            "ms_per_step": round(o["ms_per_step"], 4),
+            "workload": f"RS({o['k']},{o['m']}) encode + single-shard decode, "
+                        f"{'%d B' % o['n'] if o['n'] else 'mixed 256 B-1 MiB'} values, "
+                        f"{o['B']} stripes per GPU ({o['what']})",
+            "encode_frac": o["roofline"]["frac"], "decode_frac": o["decode_roofline"]["frac"],
+            "verified": o["verified"],
+        }
     if rank == 0:
+        k, m, n, B = r["k"], r["m"], r["n"], r["B"]
         res = {
             "metric": METRIC if args.workload == "rs32_4k" else f"GiB/s device-resident {args.workload}",
-            "value": round(value, 2),
+            "value": round(r["value"], 2),
             "unit": "GiB/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -248,36 +303,21 @@ def run_device(args):
             "data": "synthetic (uniform random bytes, torch.Generator seeded per rank)",
             "config": {
                 "workload": f"RS({k},{m}) encode + single-shard decode, "
-                            f"{'%d B' % n if n else 'mixed 256 B-1 MiB'} values, {B} stripes per GPU ({what})",
+                            f"{'%d B' % n if n else 'mixed 256 B-1 MiB'} values, {B} stripes per GPU ({r['what']})",
                 "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
-                "bytes_per_shard_per_gpu": bytes_total,
+                "bytes_per_shard_per_gpu": r["bytes_total"],
                 "parallelism": f"{world} x independent stripe batches, no collective",
                 "engine": args.engine,
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(enc_gbps, 1),
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
-                "traffic": enc_traffic,
-                "kernel": f"combine_kernel<{k},{m},{'PermEngine' if args.engine == 'perm' else 'LdsEngine'},"
-                          "kAccNone,exact> (cec_encode)",
-                "algorithmic_bytes_per_launch": enc_bytes,
-                "launch_ms": round(enc_ms, 4),
-            },
-            "decode_roofline": {
-                "achieved": round(dec_gbps, 1), "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
-                "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(dec_ms, 4),
-                "traffic": dec_traffic,
-            },
-            "verified": ok and bad == 0.0,
+            "roofline": r["roofline"],
+            "decode_roofline": r["decode_roofline"],
+            "verified": r["verified"] and all(v["verified"] for v in also.values()),
         }
+        if also:
+            res["other_workloads"] = also
         if world == 1 and not args.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(k, m, n or 4096, args.cpu_seconds)
         print(json.dumps(res), flush=True)
-    enc_plan.destroy()
-    dec_plan.destroy()
 
 
 def run_e2e(args):

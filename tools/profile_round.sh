@@ -9,7 +9,7 @@ ROUND=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline"
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline --also="
 cd /tmp && export TMPDIR=/tmp
 for W in ${PROF_WORKLOADS:-rs32_4k rs32_mixed rs42_64k rs32_1m}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$W" -o run --output-format csv \

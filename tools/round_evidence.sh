@@ -11,11 +11,12 @@ OUT=$R/gpurun_out/evidence_$ROUND
 mkdir -p "$OUT"
 cd "$R"
 B="timeout -k 10 300 python bench.py"
+BW="$B --also="  # one workload per line
 $B                                     > "$OUT/bench_default.jsonl" 2> "$OUT/bench_default.err"
-$B --no-cpu-baseline --engine lds      > "$OUT/bench_lds.jsonl"     2> "$OUT/bench_lds.err"
-$B --no-cpu-baseline --workload rs32_mixed > "$OUT/bench_mixed.jsonl" 2> "$OUT/bench_mixed.err"
-$B --no-cpu-baseline --workload rs42_64k   > "$OUT/bench_rs42.jsonl"  2> "$OUT/bench_rs42.err"
-$B --no-cpu-baseline --workload rs32_1m    > "$OUT/bench_1m.jsonl"    2> "$OUT/bench_1m.err"
+$BW --no-cpu-baseline --engine lds      > "$OUT/bench_lds.jsonl"     2> "$OUT/bench_lds.err"
+$BW --no-cpu-baseline --workload rs32_mixed > "$OUT/bench_mixed.jsonl" 2> "$OUT/bench_mixed.err"
+$BW --no-cpu-baseline --workload rs42_64k   > "$OUT/bench_rs42.jsonl"  2> "$OUT/bench_rs42.err"
+$BW --no-cpu-baseline --workload rs32_1m    > "$OUT/bench_1m.jsonl"    2> "$OUT/bench_1m.err"
 $B --e2e                               > "$OUT/bench_e2e.jsonl"     2> "$OUT/bench_e2e.err"
 $B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/bench_drain.err"
 $B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"

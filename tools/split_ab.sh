@@ -14,7 +14,7 @@ for r in $(seq "$ROUNDS"); do
   for s in $SPLITS; do
     for w in $WORKLOADS; do
       if [ "$s" = auto ]; then env=""; else env="CEC_SPLIT_SHIFT=$s"; fi
-      env $env timeout -k 10 200 python bench.py --no-cpu-baseline --workload "$w" \
+      env $env timeout -k 10 200 python bench.py --no-cpu-baseline --also= --workload "$w" \
         | sed "s/^/{\"split\": \"$s\", \"round\": $r, \"line\": /; s/\$/}/" >> "$OUT/ab.jsonl"
     done
   done
