@@ -137,3 +137,18 @@ def run_batched_case(oracle, tmp_path, K=3, M=2, units=24, seed=0xC0C70B47) -> N
     assert got.shape[0] == len(exp)
     for i, e in enumerate(exp):
         assert np.array_equal(got[i], e), i
+
+
+def run_dropin_daemon(tmp_path) -> str:
+    """tests/dropin/dropin_daemon.c: matrix + inversion, fork() (memcached's daemonize),
+    then the first region multiplies in the child; returns the child's report."""
+    exe = os.path.join(str(tmp_path), "dropin_daemon")
+    subprocess.run(
+        ["gcc", "-O1", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+         os.path.join(HERE, "dropin_daemon.c"), "-L", LIBDIR, "-lJerasure",
+         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+        check=True,
+    )
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stderr[-2000:]}\n{r.stdout}"
+    return r.stdout

@@ -592,6 +592,15 @@ def test_dropin_c_program(gpu, oracle, tmp_path):
     run_dropin_case(oracle, tmp_path)
 
 
+def test_dropin_after_daemonize_fork(gpu, tmp_path):
+    """memcached builds the matrix (memcached.c:6845) before it daemonizes with fork()
+    (:6946-6955): the shim's host-only symbols must leave the GPU untouched so that the
+    daemon child's first galois_w08_region_multiply can open it."""
+    from tests.dropin import run_dropin_daemon
+
+    assert "child 0 mismatches" in run_dropin_daemon(tmp_path)
+
+
 def test_dropin_reentrant_threads(gpu, tmp_path):
     """8 pthreads call the drop-in concurrently (all four argument forms, sizes up to
     300 KB so both the zero-copy and the staged path run, odd alignments); each checks
