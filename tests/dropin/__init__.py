@@ -9,15 +9,19 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-LIBDIR = os.path.join(ROOT, "cocytus_amd")
+# tools/asan.sh points these at a host-ASan/UBSan build of the library and compiles
+# the programs with the matching clang runtime (CEC_DROPIN_CC / CEC_DROPIN_CFLAGS).
+LIBDIR = os.environ.get("CEC_DROPIN_LIBDIR") or os.path.join(ROOT, "cocytus_amd")
+CC = os.environ.get("CEC_DROPIN_CC") or "gcc"
+XFLAGS = os.environ.get("CEC_DROPIN_CFLAGS", "").split()
 
 
 def build_dropin(out_dir: str) -> str:
     exe = os.path.join(out_dir, "dropin_main")
     subprocess.run(
-        ["gcc", "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
+        [CC, "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
          os.path.join(HERE, "dropin_main.c"), "-L", LIBDIR, "-lJerasure",
-         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+         f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
         check=True,
     )
     return exe
@@ -26,9 +30,9 @@ def build_dropin(out_dir: str) -> str:
 def run_dropin_threads(tmp_path, threads=8, iters=200) -> str:
     exe = os.path.join(str(tmp_path), "dropin_threads")
     subprocess.run(
-        ["gcc", "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
+        [CC, "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
          os.path.join(HERE, "dropin_threads.c"), "-L", LIBDIR, "-lJerasure", "-lpthread",
-         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+         f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
         check=True,
     )
     r = subprocess.run([exe, str(threads), str(iters)], capture_output=True, text=True, timeout=600)
@@ -107,9 +111,9 @@ def run_batched_case(oracle, tmp_path, K=3, M=2, units=24, seed=0xC0C70B47) -> N
             f.write(v.tobytes())
     exe = os.path.join(str(tmp_path), "batched_main")
     subprocess.run(
-        ["gcc", "-O1", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+        [CC, "-O1", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
          os.path.join(HERE, "batched_main.c"), "-L", LIBDIR, "-lcocytus_ec",
-         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+         f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
         check=True,
     )
     outp = tmp_path / "batched_out.bin"
@@ -144,9 +148,9 @@ def run_dropin_daemon(tmp_path) -> str:
     then the first region multiplies in the child; returns the child's report."""
     exe = os.path.join(str(tmp_path), "dropin_daemon")
     subprocess.run(
-        ["gcc", "-O1", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+        [CC, "-O1", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
          os.path.join(HERE, "dropin_daemon.c"), "-L", LIBDIR, "-lJerasure",
-         f"-Wl,-rpath,{LIBDIR}", "-o", exe],
+         f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
         check=True,
     )
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)

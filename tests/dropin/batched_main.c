@@ -175,6 +175,15 @@ int main(int argc, char **argv) {
     fclose(out);
     CE(cec_arenas_free(sslab));
     CE(cec_arenas_free(slab));
+    free(buf);
+    free(live);
+    free(ext);
+    free(ups);
+    free(diffs);
+    free(vals);
+    free(host);
+    free(sets);
+    free(matrix);
     printf("OK\n");
     return 0;
 }

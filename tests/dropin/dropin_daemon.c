@@ -63,6 +63,7 @@ int main(void) {
     if (pid == 0) _exit(child_work(matrix, K));
     int st = 0;
     if (waitpid(pid, &st, 0) != pid) return 6;
+    free(matrix);
     if (!WIFEXITED(st)) {
         fprintf(stderr, "daemon child died (status %d)\n", st);
         return 7;

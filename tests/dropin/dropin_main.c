@@ -99,6 +99,14 @@ int main(int argc, char **argv) {
     for (int p = 0; p < M; ++p) fwrite(parity[p], 1, arena, out);
     for (int i = 0; i < n; ++i) fwrite(rec[i], 1, nbuf, out);
     fclose(out);
+    for (int i = 0; i < n; ++i) free(rec[i]);
+    for (int i = 0; i < m; ++i) free(C[i]);
+    for (int j = 0; j < K; ++j) free(data[j]);
+    for (int p = 0; p < M; ++p) free(parity[p]);
+    free(inv);
+    free(tmpmat);
+    free(sets);
+    free(matrix); /* the server never frees it (memcached.c:6845); a test does */
     printf("dropin ok: K=%d M=%d sets=%d units=%d lost=%d\n", K, M, nsets, nunits, n);
     return 0;
 }

@@ -1,0 +1,45 @@
+#!/bin/bash
+# tools/asan.sh build|run -- the library's host code under AddressSanitizer + UBSan.
+#   build (here, on the CPU): tools/asan/libcocytus_ec.so (+ libJerasure.so), host-side
+#         instrumented only (-Xarch_host: GPU sanitizers are not available on this pool),
+#         and tools/asan/pool_bench.bin against it.
+#   run   (on the GPU box): the C programs of tests/dropin (the drop-in chain, 8-thread
+#         re-entrancy, memcached's daemonize order, the batched bindings: drainer,
+#         recovery pool) compiled with clang -fsanitize=address,undefined against that
+#         library and checked against the oracle by their pytest cases, then the idle-
+#         recoverer pool bench.  Leaks are checked; only the HIP runtime's are suppressed.
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+ROCM=${ROCM_PATH:-/opt/rocm}
+RT=$ROCM/lib/llvm/lib/clang/22/lib/linux
+A=$R/tools/asan
+SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined -Xarch_host -fno-omit-frame-pointer -shared-libsan"
+case "${1:-}" in
+build)
+  mkdir -p "$A"
+  $ROCM/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -shared -fvisibility=hidden \
+      -mcode-object-version=5 $SAN -I"$R/include" -Wl,-rpath,$ROCM/lib -Wl,-rpath,$RT \
+      -o "$A/libcocytus_ec.so" "$R/cocytus_amd/csrc/cec_runtime.hip"
+  ln -sf libcocytus_ec.so "$A/libJerasure.so"
+  $ROCM/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 $SAN "$R/tools/pool_bench.hip" \
+      -L"$A" -lcocytus_ec -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT -o "$A/pool_bench.bin"
+  ;;
+run)
+  mkdir -p "$R/gpurun_out"
+  export CEC_DROPIN_LIBDIR=$A CEC_DROPIN_CC=$ROCM/llvm/bin/clang
+  export CEC_DROPIN_CFLAGS="-g -fsanitize=address,undefined -fno-sanitize-recover=undefined -shared-libsan -Wl,-rpath,$RT"
+  export ASAN_OPTIONS=detect_leaks=1:abort_on_error=0:verify_asan_link_order=0
+  export LSAN_OPTIONS=suppressions=$R/tools/asan_lsan.supp:print_suppressions=0
+  export UBSAN_OPTIONS=print_stacktrace=1
+  cd "$R"
+  # the instrumented runtime is what the programs load (and the daemonize order under it)
+  $CEC_DROPIN_CC -std=gnu11 -I"$R/include" "$R/tests/dropin/dropin_daemon.c" -L"$A" -lJerasure \
+      -Wl,-rpath,"$A" $CEC_DROPIN_CFLAGS -o "$R/gpurun_out/dropin_daemon_asan"
+  ldd "$R/gpurun_out/dropin_daemon_asan" | grep -E "asan|Jerasure"
+  timeout -k 10 60 "$R/gpurun_out/dropin_daemon_asan"
+  timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
+      -k "dropin or batched_bindings" -p no:cacheprovider
+  timeout -k 10 200 "$A/pool_bench.bin"
+  ;;
+*) echo "usage: $0 build|run" >&2; exit 2 ;;
+esac
