@@ -67,6 +67,7 @@ struct DevInfo {
     std::once_flag once;
     int status = CEC_ENODEV;
     int cus = 256;
+    size_t lds_per_cu = 160 * 1024;  // gfx950
     char msg[256] = "";
 };
 static DevInfo g_dev[64];
@@ -93,6 +94,7 @@ static int current_device(int *dev) {
             return;
         }
         d.cus = p.multiProcessorCount > 0 ? p.multiProcessorCount : 256;
+        if (p.maxSharedMemoryPerMultiProcessor > 0) d.lds_per_cu = p.maxSharedMemoryPerMultiProcessor;
         d.status = CEC_OK;
     });
     if (d.status != CEC_OK) return fail(d.status, "%s", d.msg);
@@ -173,7 +175,7 @@ static void assign_rows(Pattern &p, std::vector<uint8_t> &rows) {
 template <int NT, int LT, class Eng, int kAcc, bool kExact>
 static void launch_k(const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
     hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid),
-                       dim3(kBlock >> a.split_shift), Eng::kStaged ? lds : 0, s, a);
+                       dim3(kBlock >> a.split_shift), lds, s, a);
 }
 
 // Exact-shape kernels for the hot ops: encode / decode / residual / solve (no RMW,
@@ -358,6 +360,26 @@ static uint32_t split_shift_for(const Streams &st, const cec_plan *plan) {
     return full && (mis & (kLineBytes - 1)) == 0 ? 2u : 0u;
 }
 
+// Waves per CU a launch may hold (0 = as many as fit).  Fewer streaming waves per CU
+// keep fewer HBM requests in flight; the cap is applied by sizing each workgroup's
+// dynamic LDS so that only cap / (waves per workgroup) workgroups fit on a CU.
+// CEC_WAVES_PER_CU overrides it (measurement).
+static std::atomic<int> g_waves_per_cu{[] {
+    const char *e = getenv("CEC_WAVES_PER_CU");
+    return e && *e ? std::max(0, atoi(e)) : 0;
+}()};
+static int waves_per_cu_cap() { return g_waves_per_cu.load(std::memory_order_relaxed); }
+
+static size_t occupancy_lds(int dev, uint32_t split_shift) {
+    const int cap = waves_per_cu_cap();
+    if (cap <= 0) return 0;
+    const int waves_per_wg = (kBlock >> split_shift) / 64;
+    const int wgs = std::max(1, cap / std::max(1, waves_per_wg));
+    const size_t per_cu = g_dev[dev].lds_per_cu;
+    const size_t lds = per_cu / static_cast<size_t>(wgs);
+    return std::min<size_t>(65536, lds > 256 ? lds - 256 : 0);  // strictly below the boundary
+}
+
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
                        uint64_t implicit_len, hipStream_t stream) {
@@ -394,16 +416,17 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     const bool lds = g_engine.load() == CEC_ENGINE_LDS;
     int max_rows = 0;
     for (const Pattern &p : pats) max_rows = std::max(max_rows, p.lds_rows);
-    const size_t lds_bytes = static_cast<size_t>(max_rows) * 256;
     a.split_shift = split_shift_for(st, plan);
+    const size_t lds_bytes = std::max(lds ? static_cast<size_t>(max_rows) * 256 : 0,
+                                      occupancy_lds(dev, a.split_shift));
     const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, 0x7FFFFFFFull));
     int en, el, eacc;
     const bool exact = exact_shape(pats, &en, &el, &eacc) &&
                        (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, lds_bytes, stream)
-                            : launch_exact<PermEngine>(en, el, eacc, a, grid, 0, stream));
+                            : launch_exact<PermEngine>(en, el, eacc, a, grid, lds_bytes, stream));
     if (!exact) {
         if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, lds_bytes, stream);
-        else launch_generic<PermEngine>(nt, lt, a, grid, 0, stream);
+        else launch_generic<PermEngine>(nt, lt, a, grid, lds_bytes, stream);
     }
     HIP_TRY(hipGetLastError());
     return CEC_OK;
@@ -513,6 +536,12 @@ CEC_API int cec_set_engine(cec_engine e) {
     return CEC_OK;
 }
 CEC_API cec_engine cec_get_engine(void) { return static_cast<cec_engine>(g_engine.load()); }
+CEC_API int cec_set_waves_per_cu(int waves_per_cu) {
+    if (waves_per_cu < 0 || waves_per_cu > 64) return fail(CEC_EINVAL, "bad waves_per_cu %d", waves_per_cu);
+    g_waves_per_cu.store(waves_per_cu);
+    return CEC_OK;
+}
+CEC_API int cec_get_waves_per_cu(void) { return waves_per_cu_cap(); }
 
 // ============================================================== ops
 CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void *dst, int add,

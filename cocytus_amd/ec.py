@@ -82,6 +82,8 @@ _SIGS = {
     "cec_device_check": ([], _i),
     "cec_set_engine": ([_i], _i),
     "cec_get_engine": ([], _i),
+    "cec_set_waves_per_cu": ([_i], _i),
+    "cec_get_waves_per_cu": ([], _i),
     "cec_plan_create": ([ctypes.POINTER(_vp), ctypes.POINTER(Extent), _i, _vp], _i),
     "cec_plan_destroy": ([_vp], _i),
     "cec_plan_num_extents": ([_vp], _i),
@@ -235,6 +237,14 @@ def set_engine(engine: int) -> None:
 
 def get_engine() -> int:
     return lib().cec_get_engine()
+
+
+def set_waves_per_cu(waves: int) -> None:
+    _check(lib().cec_set_waves_per_cu(waves))
+
+
+def get_waves_per_cu() -> int:
+    return lib().cec_get_waves_per_cu()
 
 
 def arena_stride(nbytes: int) -> int:

@@ -77,6 +77,11 @@ const char *cec_last_error(void);               /* thread-local message of the l
 int cec_device_check(void);                     /* CEC_OK if the current device is gfx950 */
 int cec_set_engine(cec_engine e);               /* process-wide; default CEC_ENGINE_PERM */
 cec_engine cec_get_engine(void);
+/* Occupancy of the streaming kernels: at most waves_per_cu waves of one launch per CU
+ * (0 = as many as fit).  Process-wide; the initial value comes from the
+ * CEC_WAVES_PER_CU environment variable.  A tuning knob: every value is bit-exact. */
+int cec_set_waves_per_cu(int waves_per_cu);
+int cec_get_waves_per_cu(void);
 
 /* ---- arena layout in HBM ----
  * The kernels stream every arena at the same offset at once.  Arenas carved from one

@@ -155,6 +155,21 @@ def test_default_engine_is_perm(lib):
     assert lib.get_engine() == lib.CEC_ENGINE_PERM
 
 
+def test_waves_per_cu_knob(lib):
+    """Occupancy cap: off by default (DESIGN.md §4 measured it and kept it off), settable,
+    range-checked; no device is needed to set it."""
+    import os
+
+    if not os.environ.get("CEC_WAVES_PER_CU"):
+        assert lib.get_waves_per_cu() == 0
+    before = lib.get_waves_per_cu()
+    lib.set_waves_per_cu(16)
+    assert lib.get_waves_per_cu() == 16
+    with pytest.raises(lib.CecError):
+        lib.set_waves_per_cu(-1)
+    lib.set_waves_per_cu(before)
+
+
 def test_headers_are_c99_and_cxx(tmp_path):
     """include/*.h compile as strict C99 (the reference server is C) and as C++."""
     src = tmp_path / "h.c"

@@ -1,0 +1,155 @@
+// tools/policy_probe.hip -- cache policy and occupancy of the encode (3 reads : 2 writes)
+// and decode (3 : 1, lost shard rotating per 4 KiB stripe) streams, in the library's
+// shape: 64-lane workgroups, one 16-B chunk per lane, arenas at the odd-4 KiB stride.
+// Not product.  Variants:
+//   * load / store cache-policy bits (gfx950 CPol: sc0 = 1, nt = 2, sc1 = 16) through
+//     raw buffer loads / stores over one resource covering the slab;
+//   * workgroups per CU capped by padding dynamic LDS (160 KiB per CU).
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/policy_probe.hip -o tools/policy_probe.bin
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t e = (x);                                                \
+        if (e != hipSuccess) {                                             \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));         \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+__device__ inline __amdgpu_buffer_rsrc_t rsrc(const void *base, uint32_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), 0, bytes, 0x00020000);
+}
+
+// ENC: arenas 0,1,2 -> 3,4.  DEC: stripe s loses data shard s % 3; reads the other two
+// data arenas and parity arena 3, writes rebuilt arena 5 + (s % 3).
+template <bool DEC, int LP, int SP>
+__global__ __launch_bounds__(64) void k_mix(const uint8_t *slab, uint32_t stride, uint32_t slab_bytes) {
+    extern __shared__ int pad[];
+    const __amdgpu_buffer_rsrc_t r = rsrc(slab, slab_bytes);
+    const uint32_t stripe = blockIdx.x >> 2;
+    const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
+    uint32_t in0, in1, in2, o0, o1;
+    if constexpr (DEC) {
+        const uint32_t lost = stripe % 3;
+        in0 = (lost == 0 ? 1 : 0) * stride;
+        in1 = (lost == 2 ? 1 : 2) * stride;
+        in2 = 3 * stride;
+        o0 = (5 + lost) * stride;
+        o1 = 0;
+    } else {
+        in0 = 0;
+        in1 = stride;
+        in2 = 2 * stride;
+        o0 = 3 * stride;
+        o1 = 4 * stride;
+    }
+    const i32x4 a = __builtin_amdgcn_raw_buffer_load_b128(r, off + in0, 0, LP);
+    const i32x4 b = __builtin_amdgcn_raw_buffer_load_b128(r, off + in1, 0, LP);
+    const i32x4 c = __builtin_amdgcn_raw_buffer_load_b128(r, off + in2, 0, LP);
+    i32x4 x = a ^ b ^ c;
+    if (pad[0] == 0x7fffffff) x.x ^= 1;  // keeps the LDS allocation (never true)
+    __builtin_amdgcn_raw_buffer_store_b128(x, r, off + o0, 0, SP);
+    if constexpr (!DEC) {
+        x.x ^= 0x1D;
+        __builtin_amdgcn_raw_buffer_store_b128(x, r, off + o1, 0, SP);
+    }
+}
+
+int main(int argc, char **argv) {
+    const uint64_t L = 256ull << 20;
+    const uint32_t stride = static_cast<uint32_t>(L + 4096);  // cec_arena_stride(L)
+    const uint32_t slab_bytes = 8u * stride;
+    uint8_t *slab;
+    CK(hipMalloc(&slab, slab_bytes));
+    for (int i = 0; i < 8; ++i)
+        hipLaunchKernelGGL(k_fill, 4096, 256, 0, 0, (uint64_t *)(slab + (uint64_t)i * stride), L / 8, 77ull + i);
+    CK(hipDeviceSynchronize());
+    struct V {
+        std::string name;
+        void (*k)(const uint8_t *, uint32_t, uint32_t);
+        bool dec;
+        int cap;  // workgroups per CU (0 = no cap)
+    };
+#define KV(D, LP, SP) (void (*)(const uint8_t *, uint32_t, uint32_t))(k_mix<D, LP, SP>)
+    std::vector<V> vs;
+    std::vector<int> caps = {32, 24, 16, 12, 8, 4};
+    const bool sweep = argc > 2;  // argv[2..]: workgroups-per-CU caps only, no policies
+    if (sweep) {
+        caps.clear();
+        for (int i = 2; i < argc; ++i) caps.push_back(atoi(argv[i]));
+    }
+    for (int d = 0; d < 2 && sweep; ++d) {
+        const bool dec = d == 1;
+        const char *w = dec ? "dec 3:1 rot" : "enc 3:2";
+        vs.push_back({std::string(w) + " nt/nt no cap [library]", dec ? KV(true, 2, 2) : KV(false, 2, 2), dec, 0});
+        for (int c : caps)
+            vs.push_back({std::string(w) + " nt/nt cap " + std::to_string(c) + " WG/CU",
+                          dec ? KV(true, 2, 2) : KV(false, 2, 2), dec, c});
+    }
+    for (int d = 0; d < 2 && !sweep; ++d) {
+        const bool dec = d == 1;
+        const char *w = dec ? "dec 3:1 rot" : "enc 3:2";
+        // policies at no cap
+        vs.push_back({std::string(w) + " ld nt    st nt    [library]", dec ? KV(true, 2, 2) : KV(false, 2, 2), dec, 0});
+        vs.push_back({std::string(w) + " ld def   st nt", dec ? KV(true, 0, 2) : KV(false, 0, 2), dec, 0});
+        vs.push_back({std::string(w) + " ld nt    st def", dec ? KV(true, 2, 0) : KV(false, 2, 0), dec, 0});
+        vs.push_back({std::string(w) + " ld def   st def", dec ? KV(true, 0, 0) : KV(false, 0, 0), dec, 0});
+        vs.push_back({std::string(w) + " ld sc0nt st nt", dec ? KV(true, 3, 2) : KV(false, 3, 2), dec, 0});
+        vs.push_back({std::string(w) + " ld nt    st sc0nt", dec ? KV(true, 2, 3) : KV(false, 2, 3), dec, 0});
+        vs.push_back({std::string(w) + " ld nt    st sc1nt", dec ? KV(true, 2, 18) : KV(false, 2, 18), dec, 0});
+        vs.push_back({std::string(w) + " ld nt    st sc0sc1nt", dec ? KV(true, 2, 19) : KV(false, 2, 19), dec, 0});
+        vs.push_back({std::string(w) + " ld sc1nt st nt", dec ? KV(true, 18, 2) : KV(false, 18, 2), dec, 0});
+        for (int c : caps)
+            if (c) vs.push_back({std::string(w) + " nt/nt cap " + std::to_string(c) + " WG/CU",
+                                 dec ? KV(true, 2, 2) : KV(false, 2, 2), dec, c});
+    }
+    const uint32_t grid = static_cast<uint32_t>(L / 1024);
+    auto launch = [&](const V &v) {
+        const size_t lds = v.cap ? (160u * 1024u) / v.cap - 256 : 4;
+        hipLaunchKernelGGL(v.k, grid, 64, lds, 0, slab, stride, slab_bytes);
+    };
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    const int rounds = argc > 1 ? atoi(argv[1]) : 7, iters = 10;
+    std::vector<std::vector<float>> ms(vs.size());
+    for (int r = 0; r < rounds; ++r)
+        for (size_t i = 0; i < vs.size(); ++i) {
+            launch(vs[i]);
+            CK(hipGetLastError());
+            CK(hipEventRecord(e0, 0));
+            for (int it = 0; it < iters; ++it) launch(vs[i]);
+            CK(hipEventRecord(e1, 0));
+            CK(hipEventSynchronize(e1));
+            float t;
+            CK(hipEventElapsedTime(&t, e0, e1));
+            ms[i].push_back(t / iters);
+        }
+    printf("64-lane workgroups, 1 KiB per WG per stream, 256 MiB per arena, odd-4KiB stride\n");
+    for (size_t i = 0; i < vs.size(); ++i) {
+        std::sort(ms[i].begin(), ms[i].end());
+        const double bytes = (vs[i].dec ? 4.0 : 5.0) * L;
+        printf("%-40s median %.4f ms -> %.0f GB/s (best %.0f)\n", vs[i].name.c_str(), ms[i][rounds / 2],
+               bytes / (ms[i][rounds / 2] * 1e6), bytes / (ms[i][0] * 1e6));
+    }
+    CK(hipFree(slab));
+    return 0;
+}
