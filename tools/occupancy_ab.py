@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """tools/occupancy_ab.py WORKLOAD CAP... -- encode / rotating-mask decode of a bench.py
 workload under cec_set_waves_per_cu caps, interleaved in one process (not product).
-Prints one line per cap: median launch us and algorithmic TB/s of encode and decode."""
+Prints one line per cap: median launch us and algorithmic TB/s of encode and decode.
+ALT=1: bench.py's step instead (encode, decode alternating, an event around each)."""
 import os
 import sys
 
@@ -34,8 +35,25 @@ ops = {
     "decode": (lambda: ec.decode(k, m, mat, masks, data + par, out, dp, s), (k + 1) * total),
 }
 res = {(c, o): [] for c in caps for o in ops}
+if os.environ.get("ALT"):  # bench.py's step: encode, decode alternating, an event around each
+    ev = [ec.Event() for _ in range(3 * 10)]
+    for rnd in range(int(os.environ.get("ROUNDS", "7"))):
+        for c in caps:
+            ec.set_waves_per_cu(c)
+            for i in range(10):
+                ev[3 * i].record(s)
+                ops["encode"][0]()
+                ev[3 * i + 1].record(s)
+                ops["decode"][0]()
+                ev[3 * i + 2].record(s)
+            torch.cuda.synchronize()
+            res[(c, "encode")].append(sum(ev[3 * i].elapsed_ms(ev[3 * i + 1]) for i in range(10)) / 10)
+            res[(c, "decode")].append(sum(ev[3 * i + 1].elapsed_ms(ev[3 * i + 2]) for i in range(10)) / 10)
+    ops_loop = 0
+else:
+    ops_loop = 1
 a, b = ec.Event(), ec.Event()
-for rnd in range(int(os.environ.get("ROUNDS", "7"))):
+for rnd in range(int(os.environ.get("ROUNDS", "7")) * ops_loop):
     for c in caps:
         ec.set_waves_per_cu(c)
         for o, (fn, _) in ops.items():
