@@ -19,7 +19,8 @@ encodes/decodes its own batch (independent stripes, no collective on the data pa
 barrier + synchronize around the timed steps, max over ranks (weak scaling).
 
 --e2e: values start and end in pinned host memory (client sockets / recovery peers):
-H2D -> kernel -> D2H pipelined over 3 HIP streams; printed as its own JSON line.
+H2D -> kernel -> D2H pipelined over --e2e-streams HIP streams; printed as its own JSON
+line.  --e2e-zero-copy: the kernels read and write the pinned host buffers directly.
 """
 from __future__ import annotations
 
@@ -59,6 +60,8 @@ def parse(argv=None):
     ap.add_argument("--ops", action="store_true",
                     help="device-resident roofline of every SURVEY §8a op (a1-a7 + fused decode)")
     ap.add_argument("--e2e-chunk", type=int, default=4096, help="stripes per pipelined chunk")
+    ap.add_argument("--e2e-zero-copy", action="store_true",
+                    help="--e2e with the kernels reading / writing pinned host memory directly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--also", default="rs32_mixed,rs32_1m,rs42_64k",
                     help="other workloads measured after the main one, reported under "
@@ -323,7 +326,7 @@ def run_device(args):
 def run_e2e(args):
     """Values start and end in pinned host memory: per chunk, H2D of the K data shards
     -> encode -> D2H of the M parities, and H2D of the K survivors (D1..D_{K-1}, P0)
-    -> decode of D0 -> D2H of the rebuilt shard; chunks round-robin over 3 streams."""
+    -> decode of D0 -> D2H of the rebuilt shard; chunks round-robin over the streams."""
     torch, dist, ec, world, rank = setup(args.dist_backend)
     k, m, n, B, _ = WORKLOADS["rs32_4k"]
     mat = ec.coding_matrix(k, m)
@@ -341,8 +344,18 @@ def run_e2e(args):
               "o": torch.empty(clen, dtype=torch.uint8, device="cuda")} for _ in streams]
     mask = ec.recovery_mask(k, m, k, [0] + [1] * (k + m - 1))  # D0 lost, leader P0
     plan = ec.Plan([(s * n, 0, n, 0) for s in range(chunk)])
+    zc_plan = ec.Plan([(s * n, 0, n, 0) for s in range(B)]) if args.e2e_zero_copy else None
+    zc_stream = torch.cuda.current_stream()
+
+    def step_zero_copy():
+        # the kernels read the values and write parity / rebuilt bytes in pinned host
+        # memory directly over PCIe: no staging copies, one launch per op
+        ec.encode(k, m, mat, data_h, par_h, zc_plan, zc_stream)
+        ec.decode(k, m, mat, [mask], data_h + par_h, [out_h, None, None], zc_plan, zc_stream)
 
     def step():
+        if args.e2e_zero_copy:
+            return step_zero_copy()
         for c in range(nch):
             st, sl = streams[c % ns], slots[c % ns]
             lo, hi = c * clen, (c + 1) * clen
@@ -390,9 +403,14 @@ def run_e2e(args):
             "ms_per_step": round(el * 1e3 / steps, 3), "verified": bool(ok),
             "h2d_bytes_per_stripe": (2 * k) * n, "d2h_bytes_per_stripe": (m + 1) * n,
             "pcie_h2d_GBps_raw": round(h2d, 1), "pcie_d2h_GBps_raw": round(d2h, 1),
-            "config": {"chunk_stripes": chunk, "streams": ns, "stripes": B},
+            "config": ({"path": "zero-copy: kernels read / write pinned host memory over PCIe",
+                        "stripes": B} if args.e2e_zero_copy else
+                       {"path": "staged: hipMemcpyAsync H2D -> kernel -> D2H",
+                        "chunk_stripes": chunk, "streams": ns, "stripes": B}),
         }), flush=True)
     plan.destroy()
+    if zc_plan is not None:
+        zc_plan.destroy()
 
 
 def run_drain(args):

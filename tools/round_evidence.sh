@@ -18,6 +18,7 @@ $BW --no-cpu-baseline --workload rs32_mixed > "$OUT/bench_mixed.jsonl" 2> "$OUT/
 $BW --no-cpu-baseline --workload rs42_64k   > "$OUT/bench_rs42.jsonl"  2> "$OUT/bench_rs42.err"
 $BW --no-cpu-baseline --workload rs32_1m    > "$OUT/bench_1m.jsonl"    2> "$OUT/bench_1m.err"
 $B --e2e                               > "$OUT/bench_e2e.jsonl"     2> "$OUT/bench_e2e.err"
+$B --e2e --e2e-zero-copy               > "$OUT/bench_e2e_zc.jsonl"  2> "$OUT/bench_e2e_zc.err"
 $B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/bench_drain.err"
 $B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"
 $B --ops                               > "$OUT/bench_ops.jsonl"     2> "$OUT/bench_ops.err"
