@@ -654,6 +654,43 @@ def test_forced_split_shift(gpu, oracle, shift):
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
 
 
+def test_pinned_host_arenas_zero_copy(gpu, oracle):
+    """bench.py --e2e-zero-copy: pinned host buffers used as arenas by the batched ops
+    (the kernels read and write them over PCIe); encode, then a decode of every mask
+    reading the parity the encode just wrote to host memory, ragged values included."""
+    torch, ec = gpu
+    k, m = 3, 2
+    rng = np.random.default_rng(77)
+    lens = [4096] * 40 + [1, 17, 4098, 300, 65536 + 5]
+    ext, arena, _ = make_extents(rng, lens)
+    mat = ec.coding_matrix(k, m)
+    host = [rng.integers(0, 256, arena, dtype=np.uint8) for _ in range(k)]
+
+    def pin(a):
+        return torch.from_numpy(a.copy()).pin_memory()
+
+    data = [pin(h) for h in host]
+    parity = [pin(np.full(arena, SENT, np.uint8)) for _ in range(m)]
+    out = [pin(np.full(arena, SENT, np.uint8)) for _ in range(k)]
+    masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
+             for p in range(m) for j in range(k)]
+    with ec.Plan([(o, 0, n, 0) for o, _, n, _ in ext]) as ep, \
+         ec.Plan([(o, 0, n, i % len(masks)) for i, (o, _, n, _) in enumerate(ext)]) as dp:
+        ec.encode(k, m, mat, data, parity, ep)
+        ec.decode(k, m, mat, masks, data + parity, out, dp)
+        torch.cuda.synchronize()
+    exp = [np.full(arena, SENT, np.uint8) for _ in range(m)]
+    for o, _, n, _ in ext:
+        seg = oracle.encode(mat, k, m, [h[o:o + n].copy() for h in host])
+        for p in range(m):
+            exp[p][o:o + n] = seg[p]
+    for p in range(m):
+        assert np.array_equal(parity[p].numpy(), exp[p]), p
+    for i, (o, _, n, _) in enumerate(ext):
+        j = [x for x in range(k) if not (masks[i % len(masks)] >> x) & 1][0]
+        assert np.array_equal(out[j].numpy()[o:o + n], host[j][o:o + n]), i
+
+
 def test_graph_capture_replay(gpu, oracle):
     """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
     bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
