@@ -327,10 +327,15 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
         if constexpr (Eng::kStaged) {
             // Stage this pattern's product rows (L2-resident, 256 B each; 512 B for an
             // RS(3,2) encode) while the stream loads above are in flight.
+            // A pattern of XORs only (coefficients 0 / 1: e.g. every decode led by the
+            // all-ones parity row) has no rows and skips the barrier; the branch is
+            // uniform over the workgroup (one tile, one pattern).
             const uint32_t nb = static_cast<uint32_t>(P->lds_rows) * 256u;
-            const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
-            for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
-            __syncthreads();
+            if (nb) {
+                const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
+                for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
+                __syncthreads();
+            }
             if (!active) continue;
         }
         compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
