@@ -111,6 +111,24 @@ def max_over_ranks(values, dist):
     return [float(x) for x in t.tolist()]
 
 
+def host_cpu() -> dict:
+    """The host the CPU baseline ran on (model, visible CPUs)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        allowed = None
+    return {"model": model, "nproc": os.cpu_count(), "affinity": allowed}
+
+
 def cpu_baseline(k, m, n, budget_s):
     """Oracle (restated Jerasure/GF-Complete, AVX2) on the host cores, bounded sample."""
     from oracle import pyoracle
@@ -130,6 +148,7 @@ def cpu_baseline(k, m, n, budget_s):
         "value": round(payload / t / 2**30, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "host": host_cpu(),
         "kind": "port",
         "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes x {reps} passes on "
                   f"{threads} threads ({t:.2f} s wall, {t * threads:.1f} thread-s); restated "
@@ -479,7 +498,7 @@ def run_drain(args):
             "pack_path": {"value": round(gib * steps / el, 2), "ms_per_step": round(el * 1e3 / steps, 3),
                           "includes": "diffs in pageable malloc'd buffers: threaded pack into pinned "
                                       "staging overlapped with H2D + fold"},
-            "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 1, "kind": "port", "host": host_cpu(),
                              "sample": "the reference's drain loop (one region multiply per diff, "
                                        "one thread) over the same 65,536 diffs, restated GF-Complete AVX2"},
         }), flush=True)
@@ -549,7 +568,7 @@ def run_recovery(args):
                         "memory: add_peer x 2 (pipelined pinned staging + fold) + solve + staged D2H. "
                         "pinned_finish: add_peer, then ONE pass for the last peer + solve, the kernel "
                         "reading and writing host memory over PCIe in both directions at once",
-            "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "cpu_baseline": {"value": round(gib / t_cpu, 3), "unit": "GiB/s", "cores": 1, "kind": "port", "host": host_cpu(),
                              "sample": "the reference's recovery chain for the same range on one thread "
                                        "(recovery.c:72-94 per unit, memcached.c:7913-7922), restated GF-Complete AVX2"},
         }), flush=True)
