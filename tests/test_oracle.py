@@ -1,6 +1,7 @@
 """CPU tests of the oracle itself (oracle/gf8_ref.c): pinned against every independent
 known answer available -- the field defined from scratch in pure Python (carry-less
-multiply mod 0x11D), SURVEY.md §8c's restated matrices, the algebraic invariants of
+multiply mod 0x11D) and through sympy's GF(2)[x] arithmetic, a second implementation of
+the big-Vandermonde construction, SURVEY.md §8c's restated matrices, the invariants of
 Jerasure's big-Vandermonde distribution matrix -- plus round trips of the reference's
 call chains and the committed golden fixtures.  (Jerasure itself is unavailable:
 parity unpinned.)"""
@@ -52,6 +53,94 @@ def test_field_against_definition(oracle):
         assert oracle.gf_exp(oracle.gf_log(a)) == a
         assert oracle.gf_mul(a, oracle.gf_div(1, a)) == 1
     assert oracle.gf_div(5, 0) == -1
+
+
+def _poly(a: int) -> list[int]:
+    """GF(2)[x] coefficient list (highest degree first) of the bit pattern a."""
+    return [int(b) for b in bin(a)[2:]] if a else []
+
+
+def _int(f) -> int:
+    return int("".join(str(int(c)) for c in f), 2) if f else 0
+
+
+def test_field_against_sympy(oracle):
+    """The field through a third-party implementation: sympy's GF(p)[x] arithmetic
+    (galoistools), product modulo x^8+x^4+x^3+x^2+1 for every pair of bytes, the
+    polynomial irreducible and x (= 2) of order 255, so the log / antilog tables the
+    reference's w = 8 region multiply is built from exist and are the oracle's."""
+    from sympy import ZZ
+    from sympy.polys import galoistools as gt
+
+    P = _poly(0x11D)
+    assert gt.gf_irreducible_p(P, 2, ZZ)
+    x = _poly(2)
+    assert _int(gt.gf_pow_mod(x, 255, P, 2, ZZ)) == 1
+    for q in (3, 5, 17):  # 255 = 3 * 5 * 17: x has full order
+        assert _int(gt.gf_pow_mod(x, 255 // q, P, 2, ZZ)) != 1
+    for i in range(255):
+        assert _int(gt.gf_pow_mod(x, i, P, 2, ZZ)) == oracle.gf_exp(i)
+    for a in range(256):
+        fa = _poly(a)
+        for b in range(256):
+            got = _int(gt.gf_rem(gt.gf_mul(fa, _poly(b), 2, ZZ), P, 2, ZZ))
+            assert oracle.gf_mul(a, b) == got, (a, b)
+
+
+def _jerasure_big_vandermonde(rows: int, cols: int) -> list[int]:
+    """Jerasure 2.x reed_sol_big_vandermonde_distribution_matrix(rows, cols, 8), written
+    again from its published algorithm with the from-scratch field above (a second
+    implementation to check the C oracle's, not the library itself):
+    the extended Vandermonde matrix (row 0 = e_0, row rows-1 = e_{cols-1}, row i = powers
+    of i), column operations to the identity on top, then coding columns scaled so row
+    `cols` is all ones, then coding rows scaled so column 0 is all ones."""
+    def inv(a):
+        return next(b for b in range(1, 256) if clmul_mod(a, b) == 1)
+
+    def pw(a, e):
+        r = 1
+        for _ in range(e):
+            r = clmul_mod(r, a)
+        return r
+
+    d = [[0] * cols for _ in range(rows)]
+    d[0][0] = 1
+    d[rows - 1][cols - 1] = 1
+    for i in range(1, rows - 1):
+        for j in range(cols):
+            d[i][j] = pw(i, j)
+    for i in range(1, cols):
+        j = next(r for r in range(i, rows) if d[r][i])
+        if j != i:
+            d[i], d[j] = d[j], d[i]
+        if d[i][i] != 1:
+            t = inv(d[i][i])
+            for r in range(rows):
+                d[r][i] = clmul_mod(t, d[r][i])
+        for j in range(cols):
+            t = d[i][j]
+            if j != i and t:
+                for r in range(rows):
+                    d[r][j] ^= clmul_mod(t, d[r][i])
+    for j in range(cols):
+        t = d[cols][j]
+        if t != 1:
+            t = inv(t)
+            for r in range(cols, rows):
+                d[r][j] = clmul_mod(t, d[r][j])
+    for r in range(cols + 1, rows):
+        t = d[r][0]
+        if t != 1:
+            t = inv(t)
+            for j in range(cols):
+                d[r][j] = clmul_mod(d[r][j], t)
+    return [v for row in d for v in row]
+
+
+@pytest.mark.parametrize("k,m", [(2, 1), (3, 2), (4, 2), (6, 3), (8, 4), (10, 4), (12, 4), (16, 8)])
+def test_big_vandermonde_second_implementation(oracle, k, m):
+    got = oracle.big_vandermonde(k + m, k)
+    assert got == _jerasure_big_vandermonde(k + m, k)
 
 
 @pytest.mark.parametrize("c", [0, 1, 2, 3, 0x80, 0x8E, 244, 245, 255])
