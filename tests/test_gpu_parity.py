@@ -691,6 +691,22 @@ def test_pinned_host_arenas_zero_copy(gpu, oracle):
         assert np.array_equal(out[j].numpy()[o:o + n], host[j][o:o + n]), i
 
 
+def test_native_metric_harness(gpu, tmp_path):
+    """tools/bench_native.c, the metric's step through the C-ABI alone (C99, no HIP
+    header, no torch): 65,536 RS(3,2) stripes encoded and decoded with rotating
+    erasures; it checks every rebuilt shard against its original itself."""
+    import json
+
+    exe = str(tmp_path / "bench_native")
+    subprocess.run(["gcc", "-O2", "-std=c99", "-D_POSIX_C_SOURCE=199309L", "-Wall", "-Werror",
+                    "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tools", "bench_native.c"),
+                    "-L", os.path.join(ROOT, "cocytus_amd"), "-lcocytus_ec",
+                    "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd"), "-o", exe], check=True)
+    r = subprocess.run([exe, "2", "1"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr + r.stdout
+    assert json.loads(r.stdout)["verified"] is True
+
+
 def test_graph_capture_replay(gpu, oracle):
     """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
     bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
