@@ -13,9 +13,10 @@
 // coefficients (per source shard for diff-update, per erasure mask for decode).
 //
 // Hardware mapping (MI355X):
-//   * 256-thread workgroups, one 16-byte chunk per lane per tile: every stream of
-//     a tile is read with one fully coalesced global_load_dwordx4 per lane
-//     (uniform SGPR base + per-lane VGPR offset);
+//   * one 16-byte chunk per lane: a 4 KiB tile is 256 lanes, as one 256-lane
+//     workgroup or (full, line-aligned tiles) four one-wave workgroups of 64
+//     (split_shift); every stream of a tile is read with one fully coalesced
+//     global_load_dwordx4 per lane (uniform SGPR base + per-lane VGPR offset);
 //   * tile metadata and coefficient tables are wave-uniform and live in SGPRs
 //     (constant-address-space loads -> s_load);
 //   * GF multiply by a uniform coefficient c on 4 packed bytes:
