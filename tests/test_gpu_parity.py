@@ -691,6 +691,64 @@ def test_pinned_host_arenas_zero_copy(gpu, oracle):
         assert np.array_equal(out[j].numpy()[o:o + n], host[j][o:o + n]), i
 
 
+def test_registered_host_arena_zero_copy(gpu, oracle):
+    """an arena left in malloc'd host memory, registered once with
+    hipHostRegister(mapped), used through its device alias as the parity arena of
+    cec_apply_diffs (the parity server's drain) and as the data arenas of cec_encode."""
+    import ctypes
+
+    torch, ec = gpu
+    rt = sorted(ec._hip_runtimes())
+    assert len(rt) == 1, rt
+    hip = ctypes.CDLL(rt[0])
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostGetDevicePointer.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    k, m, n, B = 3, 2, 4096, 64
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(5)
+    def page_aligned(nbytes):
+        raw = np.empty(nbytes + 4096, np.uint8)
+        o = (-raw.ctypes.data) % 4096
+        return raw[o:o + nbytes]
+
+    arenas = []
+    for _ in range(k + m):
+        a = page_aligned(B * n)
+        a[:] = rng.integers(0, 256, B * n, dtype=np.uint8)
+        arenas.append(a)
+    orig = [a.copy() for a in arenas]
+    alias = []
+    try:
+        for a in arenas:
+            assert hip.hipHostRegister(a.ctypes.data, a.nbytes, 2) == 0  # hipHostRegisterMapped
+            d = ctypes.c_void_p()
+            assert hip.hipHostGetDevicePointer(ctypes.byref(d), a.ctypes.data, 0) == 0
+            alias.append(d.value)
+        with ec.Plan([(s * n, 0, n, 0) for s in range(B)]) as ep:
+            ec.encode(k, m, mat, alias[:k], alias[k:], ep)
+            torch.cuda.synchronize()
+        exp = oracle.encode(mat, k, m, orig[:k])
+        for p in range(m):
+            assert np.array_equal(arenas[k + p], exp[p]), p
+        # a drain of shipped diffs into the registered parity arena P1 (lid k + 1)
+        diffs = rng.integers(0, 256, B * n, dtype=np.uint8)
+        ddev = to_dev(torch, diffs)
+        ext = [(s * n, s * n, n, s % k) for s in range(B)]
+        want = arenas[k + 1].copy()
+        for off, soff, ln, j in ext:
+            w = want[off:off + ln].copy()
+            oracle.parity_apply(mat, k, k + 1, j, diffs[soff:soff + ln].copy(), w)
+            want[off:off + ln] = w
+        with ec.Plan(ext) as ap:
+            ec.apply_diffs(k, m, mat, k + 1, ddev, alias[k + 1], ap)
+            torch.cuda.synchronize()
+        assert np.array_equal(arenas[k + 1], want)
+    finally:
+        for a in arenas[:len(alias)]:
+            hip.hipHostUnregister(a.ctypes.data)
+
+
 def test_native_metric_harness(gpu, tmp_path):
     """tools/bench_native.c, the metric's step through the C-ABI alone (C99, no HIP
     header, no torch): 65,536 RS(3,2) stripes encoded and decoded with rotating
