@@ -70,3 +70,21 @@ def test_layouts():
     assert all(256 <= ln <= 1 << 20 for _, ln in s)
     assert all(a[0] + a[1] <= b[0] for a, b in zip(s, s[1:]))  # no overlap
     assert bench.layout("rs32_mixed") == (s, arena)  # seeded
+
+
+def test_bench_arguments():
+    """The driver's contract: no flags = N=1, the metric's workload, steps/warmup that
+    finish in minutes; the other device-resident configs ride along (--also)."""
+    import bench
+
+    a = bench.parse([])
+    assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "perm")
+    assert 1 <= a.steps <= 100 and a.warmup >= 1
+    assert set(a.also.split(",")) == {"rs32_mixed", "rs32_1m", "rs42_64k"}
+    assert bench.parse(["--also="]).also == ""
+    with pytest.raises(SystemExit):
+        bench.parse(["--also=rs99"])
+    a = bench.parse(["--gpus", "8", "--steps", "7", "--warmup", "2"])
+    assert (a.gpus, a.steps, a.warmup) == (8, 7, 2)
+    h = bench.host_cpu()
+    assert h["nproc"] >= 1 and isinstance(h["model"], str)
