@@ -14,9 +14,13 @@ algorithmic HBM bytes ((K+M)*n per stripe) per launch / its HIP-event launch tim
 cpu_baseline = the oracle's restated Jerasure/GF-Complete path (AVX2 split-nibble), on
 the host cores, same chaining as the reference's call sites.
 
-Multi-GPU: `torch.distributed.run --nproc-per-node N bench.py --gpus N`: every rank
+Multi-GPU: `bench.py --gpus N` starts N rank processes itself (torch.distributed.run as
+a child, before anything touches the GPU), or runs as one rank of an outer
+`torch.distributed.run --nproc-per-node N bench.py --gpus N`: every rank
 encodes/decodes its own batch (independent stripes, no collective on the data path);
 barrier + synchronize around the timed steps, max over ranks (weak scaling).
+other_workloads also carries the fused per-SET diff-update (the north star's first op)
+and the pinned-host end-to-end path, each with its own roofline / PCIe fraction.
 
 --e2e: values start and end in pinned host memory (client sockets / recovery peers):
 H2D -> kernel -> D2H pipelined over --e2e-streams HIP streams; printed as its own JSON
@@ -44,6 +48,13 @@ WORKLOADS = {
     "rs42_64k": (4, 2, 65536, 16384, "BASELINE configs[3], per GPU"),
     "rs32_1m": (3, 2, 1 << 20, 1024, "BASELINE configs[4] sizes"),
 }
+# Other north-star paths measured beside the encode + decode workloads (--also).
+EXTRA_WORKLOADS = {
+    "rs32_diff_update": "per-SET diff-update fused with install (SURVEY §8a a4: memcached.c:2664-2710 "
+                        "data side + 7739-7798 parity side), 65,536 x 4 KiB SETs, device-resident",
+    "rs32_e2e": "RS(3,2) 4 KiB encode + decode, values from and back to pinned host memory "
+                "(H2D -> kernels -> D2H pipelined over HIP streams)",
+}
 
 
 def parse(argv=None):
@@ -63,16 +74,24 @@ def parse(argv=None):
     ap.add_argument("--e2e-zero-copy", action="store_true",
                     help="--e2e with the kernels reading / writing pinned host memory directly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--also", default="rs32_mixed,rs32_1m,rs42_64k",
+    ap.add_argument("--harness-check", action="store_true",
+                    help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
+                         "barriers, max over ranks")
+    ap.add_argument("--also", default="rs32_mixed,rs32_1m,rs42_64k,rs32_diff_update,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
-    ap.add_argument("--cpu-seconds", type=float, default=30.0, help="CPU work budget (thread-seconds)")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="process-group backend for the barrier / max-over-ranks (nccl = RCCL)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="wall-clock budget of the CPU-baseline thread sweep (seconds)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="process-group backend for the barrier / max-over-ranks (nccl = RCCL; "
+                         "auto = nccl, or gloo when CEC_BENCH_DEVICE pins every rank to one card)")
     args = ap.parse_args(argv)
-    bad = [w for w in args.also.split(",") if w and w not in WORKLOADS]
+    if args.dist_backend == "auto":
+        args.dist_backend = "gloo" if os.environ.get("CEC_BENCH_DEVICE") else "nccl"
+    bad = [w for w in args.also.split(",") if w and w not in WORKLOADS and w not in EXTRA_WORKLOADS]
     if bad:
-        ap.error(f"--also: unknown workload(s) {bad}; choose from {sorted(WORKLOADS)}")
+        ap.error(f"--also: unknown workload(s) {bad}; choose from "
+                 f"{sorted(WORKLOADS) + sorted(EXTRA_WORKLOADS)}")
     return args
 
 
@@ -126,34 +145,75 @@ def host_cpu() -> dict:
         allowed = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
         allowed = None
-    return {"model": model, "nproc": os.cpu_count(), "affinity": allowed}
+    return {"model": model, "nproc": os.cpu_count(), "affinity": allowed, "cpu_quota": cpu_quota()}
 
 
-def cpu_baseline(k, m, n, budget_s):
-    """Oracle (restated Jerasure/GF-Complete, AVX2) on the host cores, bounded sample."""
+def cpu_quota():
+    """CPUs this process's cgroup may use (cpu.max / cfs quota), None if unlimited.  A
+    shared GPU box grants one GPU's share of the host: more threads than that only
+    time-slice."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(float(q) / float(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = float(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_thread_counts(allowed: int) -> list[int]:
+    """SURVEY §8d sweep: 1 (the reference's own configuration: one worker thread per
+    server process, memcached.c:6990), 16, 64 and every CPU this process may run on."""
+    return sorted({t for t in (1, 16, 64, allowed) if 1 <= t <= allowed})
+
+
+def cpu_baseline(k, m, n, wall_s, threads_list=None):
+    """Oracle (restated Jerasure/GF-Complete, AVX2) on the host cores, bounded samples.
+
+    One pthread per CPU on disjoint stripes, swept over cpu_thread_counts(); each
+    point runs about wall_s / len(sweep) seconds.  `value` / `cores` is the all-CPU
+    point (the host's ceiling); `reference_config` is the 1-thread point."""
     from oracle import pyoracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
-    threads = max(1, min(threads, 16))
-    stripes = max(threads, (64 << 20) // n)  # 64 MiB per shard: larger than the host LLC
-    pyoracle.bench_encode_decode(k, m, n, stripes, threads, 1, True)  # first touch
-    t1 = pyoracle.bench_encode_decode(k, m, n, stripes, threads, 4, True) / 4  # calibrate
-    reps = max(1, min(2000, int(budget_s / max(t1 * threads, 1e-6))))
-    t = pyoracle.bench_encode_decode(k, m, n, stripes, threads, reps, True)
-    payload = (k + 1) * n * stripes * reps
+    h = host_cpu()
+    allowed = h["affinity"] or os.cpu_count() or 1
+    if h["cpu_quota"]:  # threads beyond the cgroup's CPU quota only time-slice
+        allowed = max(1, min(allowed, math.ceil(h["cpu_quota"])))
+    counts = threads_list or cpu_thread_counts(allowed)
+    per_point = max(0.2, wall_s / len(counts))
+    stripes = (256 << 20) // n  # 256 MiB per shard, 1.25 GiB for RS(3,2): above any LLC
+    simd = "AVX2" if pyoracle.simd_available() else "scalar"
+    sweep = []
+    for T in counts:
+        t1 = pyoracle.bench_encode_decode(k, m, n, stripes, T, 1, True)  # calibrate (fill untimed)
+        reps = max(1, min(1000, int(per_point / max(t1, 1e-6))))
+        t = pyoracle.bench_encode_decode(k, m, n, stripes, T, reps, True)
+        sweep.append({"threads": T, "value": round((k + 1) * n * stripes * reps / t / 2**30, 3),
+                      "wall_s": round(t, 2), "passes": reps})
+    top = sweep[-1]
     from oracle import jerasure_probe
 
     ref_lib, where = jerasure_probe.load()  # SURVEY §8d: probe for the real library
     return {
-        "value": round(payload / t / 2**30, 3),
+        "value": top["value"],
         "unit": "GiB/s",
-        "cores": threads,
-        "host": host_cpu(),
+        "cores": top["threads"],
+        "host": h,
         "kind": "port",
-        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes x {reps} passes on "
-                  f"{threads} threads ({t:.2f} s wall, {t * threads:.1f} thread-s); restated "
-                  f"GF-Complete SPLIT(8,4) split-nibble ({'AVX2' if pyoracle.simd_available() else 'scalar'}), "
-                  "chained like memcached.c/recovery.c",
+        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes, {top['passes']} passes on "
+                  f"{top['threads']} threads ({top['wall_s']:.2f} s wall): every CPU this process may use "
+                  f"(affinity {h['affinity']}, cgroup quota {h['cpu_quota']}), the host's ceiling for it; "
+                  f"restated GF-Complete SPLIT(8,4) split-nibble ({simd}), chained like memcached.c/recovery.c",
+        "reference_config": dict(sweep[0], note="1 thread: the reference's configuration, one worker "
+                                                "thread per server process (memcached.c:6990)"),
+        "sweep": sweep,
         "reference_probe": f"system libJerasure found at {where} (pins the oracle: tests/test_oracle.py)"
                            if ref_lib is not None else where,
     }
@@ -291,6 +351,182 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
     }
 
 
+def measure_diff_update(torch, dist, ec, world, rank, args):
+    """The north star's first op on device-resident arenas: 65,536 SETs of 4 KiB per GPU,
+    source shard j uniform in {0,1,2}, one cec_diff_update launch per step
+    (d = new ^ old; P_p ^= MATRIX(K+p, j) * d for both parities; old := new).  Steps
+    alternate between two staging batches so every step changes every value.  Check
+    (size-independent): afterwards parity == encode(data), on the device."""
+    k, m, n, B = 3, 2, 4096, 65536
+    T = n * B
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70006 + rank)
+    ar = ec.arena_tensors(k + m + 2, T)
+    data, parity, stage = ar[:k], ar[k:k + m], ar[k + m:]
+    for t in data + stage:
+        t.random_(0, 256, generator=g)
+    src = torch.randint(0, k, (B,), generator=torch.Generator().manual_seed(0xC0C70006 + rank)).tolist()
+    plan = ec.Plan([(s * n, s * n, n, src[s]) for s in range(B)])
+    stream = torch.cuda.current_stream()
+    ec.encode_region(k, m, mat, data, parity, T, stream)
+    for w in range(args.warmup):
+        ec.diff_update(k, m, mat, data, stage[w % 2], parity, True, plan, stream)
+    evs = [ec.Event() for _ in range(args.steps + 1)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    evs[0].record(stream)
+    for s in range(args.steps):
+        ec.diff_update(k, m, mat, data, stage[(args.warmup + s) % 2], parity, True, plan, stream)
+        evs[s + 1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    ms = sum(evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)) / args.steps
+    chk = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, chk, T, stream)
+    torch.cuda.synchronize()
+    ok = all(torch.equal(chk[p], parity[p]) for p in range(m))
+    elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist)
+    plan.destroy()
+    del ar, data, parity, stage, chk
+    nbytes = (2 + 2 * m + 1) * T  # read old, new, M parities; write M parities + install
+    gbps = nbytes / (ms * 1e-3) / 1e9
+    return {
+        "value": round(T * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
+        "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+        "workload": f"RS(3,2) {EXTRA_WORKLOADS['rs32_diff_update']}; value = SET payload (n per SET)",
+        "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                     "frac": round(gbps / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": nbytes,
+                     "launch_ms": round(ms, 4),
+                     "kernel": "combine_kernel<2,3,*,kAccAllButLast,exact> (cec_diff_update, install)",
+                     "traffic": load_traffic("rs32_diff_update")[0]},
+        "verified": bool(ok and bad == 0.0),
+    }
+
+
+def pcie_raw(torch, nbytes=256 << 20, reps=4):
+    """Raw pinned H2D / D2H copy rates of this GPU's link (GB/s)."""
+    x = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
+    y = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    y.copy_(x, non_blocking=True)
+    torch.cuda.synchronize()
+    rates = []
+    for a, b in ((y, x), (x, y)):
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            a.copy_(b, non_blocking=True)
+        torch.cuda.synchronize()
+        rates.append(reps * nbytes / (time.perf_counter() - t1) / 1e9)
+    return rates[0], rates[1]
+
+
+class E2E:
+    """RS(3,2) 4 KiB encode + decode with the values in pinned host memory.
+
+    Staged (default): per chunk of stripes, H2D of the K data shards -> encode -> D2H of
+    the M parities, and H2D of the K survivors (D1..D_{K-1}, P0) -> decode of D0 -> D2H
+    of the rebuilt shard; chunks round-robin over HIP streams.  Zero-copy: the kernels
+    read and write the pinned host buffers over PCIe, one launch per op."""
+
+    def __init__(self, torch, ec, args, zero_copy=False):
+        self.torch, self.ec = torch, ec
+        self.k, self.m, self.n, self.B, _ = WORKLOADS["rs32_4k"]
+        k, m, n, B = self.k, self.m, self.n, self.B
+        self.mat = ec.coding_matrix(k, m)
+        self.chunk = args.e2e_chunk  # stripes per chunk (4096: 16 MiB per shard)
+        self.ns = args.e2e_streams
+        self.zero_copy = zero_copy
+        clen = self.chunk * n
+        pin = dict(dtype=torch.uint8, pin_memory=True)
+        self.data_h = [torch.randint(0, 256, (B * n,), dtype=torch.uint8).pin_memory() for _ in range(k)]
+        self.par_h = [torch.empty(B * n, **pin) for _ in range(m)]
+        self.out_h = torch.empty(B * n, **pin)
+        self.streams = [torch.cuda.Stream() for _ in range(self.ns)]
+        self.slots = [{"d": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(k)],
+                       "p": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(m)],
+                       "o": torch.empty(clen, dtype=torch.uint8, device="cuda")} for _ in self.streams]
+        self.mask = ec.recovery_mask(k, m, k, [0] + [1] * (k + m - 1))  # D0 lost, leader P0
+        self.plan = ec.Plan([(s * n, 0, n, 0) for s in range(self.chunk)])
+        self.zc_plan = ec.Plan([(s * n, 0, n, 0) for s in range(B)]) if zero_copy else None
+        self.h2d_bytes = 2 * k * n * B  # per step: K data shards, then K survivors
+        self.d2h_bytes = (m + 1) * n * B  # M parities + the rebuilt shard
+        self.payload = (k + 1) * n * B  # K*n encoded + n rebuilt per stripe (the metric's)
+
+    def step(self):
+        torch, ec, k, m = self.torch, self.ec, self.k, self.m
+        if self.zero_copy:
+            s = torch.cuda.current_stream()
+            ec.encode(k, m, self.mat, self.data_h, self.par_h, self.zc_plan, s)
+            ec.decode(k, m, self.mat, [self.mask], self.data_h + self.par_h, [self.out_h, None, None],
+                      self.zc_plan, s)
+            return
+        clen = self.chunk * self.n
+        for c in range(self.B // self.chunk):
+            st, sl = self.streams[c % self.ns], self.slots[c % self.ns]
+            lo, hi = c * clen, (c + 1) * clen
+            with torch.cuda.stream(st):
+                for j in range(k):
+                    sl["d"][j].copy_(self.data_h[j][lo:hi], non_blocking=True)
+                ec.encode(k, m, self.mat, sl["d"], sl["p"], self.plan, st)
+                for p in range(m):
+                    self.par_h[p][lo:hi].copy_(sl["p"][p], non_blocking=True)
+                for j in range(1, k):  # survivors arrive again from the peers
+                    sl["d"][j].copy_(self.data_h[j][lo:hi], non_blocking=True)
+                sl["p"][0].copy_(self.par_h[0][lo:hi], non_blocking=True)
+                ec.decode(k, m, self.mat, [self.mask], sl["d"] + sl["p"], [sl["o"], None, None],
+                          self.plan, st)
+                self.out_h[lo:hi].copy_(sl["o"], non_blocking=True)
+
+    def verified(self):
+        return bool(self.torch.equal(self.out_h, self.data_h[0]))
+
+    def close(self):
+        self.plan.destroy()
+        if self.zc_plan is not None:
+            self.zc_plan.destroy()
+
+
+def measure_e2e(torch, dist, ec, world, rank, args):
+    """E2E (staged) beside the device-resident workloads, barrier + max over ranks (each
+    GPU has its own PCIe link: weak scaling).  pcie_bound_frac = the step's PCIe floor
+    max(H2D bytes / raw H2D, D2H bytes / raw D2H) over the measured step time."""
+    e = E2E(torch, ec, args)
+    for _ in range(max(1, args.warmup)):
+        e.step()
+    torch.cuda.synchronize()
+    ok = e.verified()
+    steps = max(1, min(args.steps, 10))
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        e.step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    h2d, d2h = pcie_raw(torch)
+    floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
+    el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
+    out = {
+        "value": round(e.payload * world * steps / el / 2**30, 2), "unit": "GiB/s",
+        "ms_per_step": round(el * 1e3 / steps, 3), "steps": steps,
+        "workload": f"{EXTRA_WORKLOADS['rs32_e2e']}; 65,536 stripes per GPU, {e.chunk}-stripe chunks "
+                    f"over {e.ns} streams",
+        "pcie_bound_frac": round(floor_s / (el / steps), 4),
+        "pcie_GBps_raw": {"h2d": round(h2d, 1), "d2h": round(d2h, 1)},
+        "h2d_bytes_per_step": e.h2d_bytes, "d2h_bytes_per_step": e.d2h_bytes,
+        "verified": bool(ok and bad == 0.0),
+    }
+    e.close()
+    return out
+
+
 def run_device(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
     ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
@@ -301,6 +537,12 @@ def run_device(args):
     also = {}
     for w in [x for x in args.also.split(",") if x and x != args.workload]:
         torch.cuda.empty_cache()
+        if w == "rs32_diff_update":
+            also[w] = measure_diff_update(torch, dist, ec, world, rank, args)
+            continue
+        if w == "rs32_e2e":
+            also[w] = measure_e2e(torch, dist, ec, world, rank, args)
+            continue
         o = measure_device(torch, dist, ec, world, rank, w, args)
         also[w] = {
             "value": round(o["value"], 2), "unit": "GiB/s",
@@ -346,93 +588,35 @@ def run_device(args):
 
 
 def run_e2e(args):
-    """Values start and end in pinned host memory: per chunk, H2D of the K data shards
-    -> encode -> D2H of the M parities, and H2D of the K survivors (D1..D_{K-1}, P0)
-    -> decode of D0 -> D2H of the rebuilt shard; chunks round-robin over the streams."""
+    """--e2e: the E2E pipeline alone, printed as its own JSON line (1 GPU)."""
     torch, dist, ec, world, rank = setup(args.dist_backend)
-    k, m, n, B, _ = WORKLOADS["rs32_4k"]
-    mat = ec.coding_matrix(k, m)
-    chunk = args.e2e_chunk  # stripes per chunk (4096: 16 MiB per shard)
-    ns = args.e2e_streams
-    nch = B // chunk
-    clen = chunk * n
-    pin = dict(dtype=torch.uint8, pin_memory=True)
-    data_h = [torch.randint(0, 256, (B * n,), dtype=torch.uint8).pin_memory() for _ in range(k)]
-    par_h = [torch.empty(B * n, **pin) for _ in range(m)]
-    out_h = torch.empty(B * n, **pin)
-    streams = [torch.cuda.Stream() for _ in range(ns)]
-    slots = [{"d": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(k)],
-              "p": [torch.empty(clen, dtype=torch.uint8, device="cuda") for _ in range(m)],
-              "o": torch.empty(clen, dtype=torch.uint8, device="cuda")} for _ in streams]
-    mask = ec.recovery_mask(k, m, k, [0] + [1] * (k + m - 1))  # D0 lost, leader P0
-    plan = ec.Plan([(s * n, 0, n, 0) for s in range(chunk)])
-    zc_plan = ec.Plan([(s * n, 0, n, 0) for s in range(B)]) if args.e2e_zero_copy else None
-    zc_stream = torch.cuda.current_stream()
-
-    def step_zero_copy():
-        # the kernels read the values and write parity / rebuilt bytes in pinned host
-        # memory directly over PCIe: no staging copies, one launch per op
-        ec.encode(k, m, mat, data_h, par_h, zc_plan, zc_stream)
-        ec.decode(k, m, mat, [mask], data_h + par_h, [out_h, None, None], zc_plan, zc_stream)
-
-    def step():
-        if args.e2e_zero_copy:
-            return step_zero_copy()
-        for c in range(nch):
-            st, sl = streams[c % ns], slots[c % ns]
-            lo, hi = c * clen, (c + 1) * clen
-            with torch.cuda.stream(st):
-                for j in range(k):
-                    sl["d"][j].copy_(data_h[j][lo:hi], non_blocking=True)
-                ec.encode(k, m, mat, sl["d"], sl["p"], plan, st)
-                for p in range(m):
-                    par_h[p][lo:hi].copy_(sl["p"][p], non_blocking=True)
-                for j in range(1, k):  # survivors arrive again from the peers
-                    sl["d"][j].copy_(data_h[j][lo:hi], non_blocking=True)
-                sl["p"][0].copy_(par_h[0][lo:hi], non_blocking=True)
-                ec.decode(k, m, mat, [mask], sl["d"] + sl["p"], [sl["o"], None, None], plan, st)
-                out_h[lo:hi].copy_(sl["o"], non_blocking=True)
-
+    e = E2E(torch, ec, args, zero_copy=args.e2e_zero_copy)
     for _ in range(max(1, args.warmup)):
-        step()
+        e.step()
     torch.cuda.synchronize()
-    ok = torch.equal(out_h, data_h[0])
+    ok = e.verified()
     steps = max(1, min(args.steps, 10))
     t0 = time.perf_counter()
     for _ in range(steps):
-        step()
+        e.step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    # raw copy rates for context
-    x = torch.empty(256 << 20, **pin)
-    y = torch.empty(256 << 20, dtype=torch.uint8, device="cuda")
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    for _ in range(4):
-        y.copy_(x, non_blocking=True)
-    torch.cuda.synchronize()
-    h2d = 4 * (256 << 20) / (time.perf_counter() - t1) / 1e9
-    t1 = time.perf_counter()
-    for _ in range(4):
-        x.copy_(y, non_blocking=True)
-    torch.cuda.synchronize()
-    d2h = 4 * (256 << 20) / (time.perf_counter() - t1) / 1e9
-    payload = (k + 1) * B * n * steps
+    h2d, d2h = pcie_raw(torch)  # raw copy rates for context
+    floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
     if rank == 0:
         print(json.dumps({
             "metric": "GiB/s end-to-end (pinned host -> HBM -> host) RS(3,2) encode+decode, 4 KiB values",
-            "value": round(payload / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
-            "ms_per_step": round(el * 1e3 / steps, 3), "verified": bool(ok),
-            "h2d_bytes_per_stripe": (2 * k) * n, "d2h_bytes_per_stripe": (m + 1) * n,
+            "value": round(e.payload * steps / el / 2**30, 2), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+            "ms_per_step": round(el * 1e3 / steps, 3), "verified": ok,
+            "h2d_bytes_per_stripe": 2 * e.k * e.n, "d2h_bytes_per_stripe": (e.m + 1) * e.n,
             "pcie_h2d_GBps_raw": round(h2d, 1), "pcie_d2h_GBps_raw": round(d2h, 1),
+            "pcie_bound_frac": round(floor_s / (el / steps), 4),
             "config": ({"path": "zero-copy: kernels read / write pinned host memory over PCIe",
-                        "stripes": B} if args.e2e_zero_copy else
+                        "stripes": e.B} if args.e2e_zero_copy else
                        {"path": "staged: hipMemcpyAsync H2D -> kernel -> D2H",
-                        "chunk_stripes": chunk, "streams": ns, "stripes": B}),
+                        "chunk_stripes": e.chunk, "streams": e.ns, "stripes": e.B}),
         }), flush=True)
-    plan.destroy()
-    if zc_plan is not None:
-        zc_plan.destroy()
+    e.close()
 
 
 def run_drain(args):
@@ -717,11 +901,77 @@ def run_ops(args):
         pl.destroy()
 
 
-def main():
-    args = parse()
-    if args.gpus > 1 and int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run --nproc-per-node N")
-    if args.e2e:
+def free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args, argv) -> int:
+    """`bench.py --gpus N` (N > 1) started without a torch.distributed.run parent: start
+    the N rank processes, one per GPU, and relay their output.  This process touches no
+    GPU (nothing here initialises HIP) and does not exec: the ranks are children, and
+    it exits with their launcher's code.  Rank 0 prints the JSON line."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1", f"--master-port={free_port()}",
+           os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on these hosts
+    # stdout carries only the JSON line(s); the launcher's and the process groups' chatter
+    # (gloo prints connection notes on stdout) goes to stderr, line by line as it comes.
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return p.wait()
+
+
+def run_harness_check(args):
+    """--harness-check: the multi-rank harness without a GPU (gloo): each rank takes its
+    contiguous shard of the metric's 65,536 stripes, barriers, times a CPU stand-in step
+    and reports max-over-ranks exactly as the device path does.  For the CPU tests."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    lo, hi = shard_range(WORKLOADS["rs32_4k"][3] * world, rank, world)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.01 * (rank + 1))  # ranks finish at different times: the max must win
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    mine = [float(elapsed), float(0.01 * (rank + 1)), float(rank)]
+    got = max_over_ranks(mine, dist if world > 1 else None)
+    spans = [None] * world
+    if world > 1:
+        dist.all_gather_object(spans, (rank, lo, hi))
+    else:
+        spans = [(0, lo, hi)]
+    if rank == 0:
+        print(json.dumps({"harness_check": True, "n_gpus": world, "gpus_arg": args.gpus,
+                          "elapsed_max": got[0], "slowest_sleep": got[1], "max_rank": got[2],
+                          "shards": spans, "local_rank_env": os.environ.get("LOCAL_RANK"),
+                          "backend": "gloo"}), flush=True)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args, argv))
+    if args.gpus > 1 and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={os.environ['WORLD_SIZE']}")
+    if args.harness_check:
+        run_harness_check(args)
+    elif args.e2e:
         run_e2e(args)
     elif args.drain:
         run_drain(args)

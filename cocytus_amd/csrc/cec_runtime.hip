@@ -101,36 +101,7 @@ static int current_device(int *dev) {
     return CEC_OK;
 }
 
-// ============================================================== pattern cache
-// Coefficient tables are small and reused for every launch of an op with the same
-// code; they are uploaded once per (device, content) and kept for the process.
-struct PatternCache {
-    std::mutex mu;
-    std::map<std::string, Pattern *> map;
-};
-static PatternCache g_pcache[64];
-
-// Patterns and the LDS engine's product rows are uploaded as one blob: rows follow
-// the patterns (16-B aligned: sizeof(Pattern) is a multiple of 16).
-static int upload_patterns(int dev, const std::vector<Pattern> &pats, const std::vector<uint8_t> &rows,
-                           const Pattern **out) {
-    std::string key(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
-    key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
-    PatternCache &c = g_pcache[dev];
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto it = c.map.find(key);
-    if (it != c.map.end()) {
-        *out = it->second;
-        return CEC_OK;
-    }
-    Pattern *d = nullptr;
-    if (hipMalloc(&d, key.size()) != hipSuccess)
-        return fail(CEC_ENOMEM, "hipMalloc(%zu) for coefficient tables failed", key.size());
-    HIP_TRY(hipMemcpy(d, key.data(), key.size(), hipMemcpyHostToDevice));
-    c.map.emplace(std::move(key), d);
-    *out = d;
-    return CEC_OK;
-}
+#include "cec_cache.inc"
 
 static Pattern blank_pattern() {
     Pattern p;
@@ -186,7 +157,7 @@ static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, 
                          hipStream_t s) {
 #define CEC_X(N, L, A)                                           \
     if (n == N && l == L && acc == A) {                          \
-        launch_k<N, L, Eng, A, true>(a, grid, lds, s);           \
+        launch_k<N, L, Eng, A, true>(a, grid, lds, s);       \
         return true;                                             \
     }
 #define CEC_XL(N) CEC_X(N, 1, kAccNone) CEC_X(N, 2, kAccNone) CEC_X(N, 3, kAccNone) CEC_X(N, 4, kAccNone)
@@ -202,7 +173,7 @@ static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, 
 // Capacity kernels for every other shape (guarded, per-pattern counts and modes).
 template <class Eng>
 static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
-#define CEC_G(NT)                                                                    \
+#define CEC_G(NT)                                                                        \
     if (lt <= 1) launch_k<NT, 1, Eng, kAccRuntime, false>(a, grid, lds, s);          \
     else if (lt <= 2) launch_k<NT, 2, Eng, kAccRuntime, false>(a, grid, lds, s);     \
     else launch_k<NT, 4, Eng, kAccRuntime, false>(a, grid, lds, s);
@@ -213,22 +184,31 @@ static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, size_
 #undef CEC_G
 }
 
-// Shape class of a pattern set: exact (n_in, n_out, acc) if all patterns agree.
-static bool exact_shape(const std::vector<Pattern> &pats, int *n, int *l, int *acc) {
-    const Pattern &p0 = pats[0];
-    for (const Pattern &p : pats) {
-        if (p.n_in != p0.n_in || p.n_out != p0.n_out) return false;
+// Shape class of the patterns a launch uses (`used`: pattern indices its tiles name;
+// NULL = all): exact (n_in, n_out, acc) if they all agree.
+static bool exact_shape(const std::vector<Pattern> &pats, const std::vector<char> *used, int *n, int *l,
+                        int *acc) {
+    const Pattern *p0 = nullptr;
+    for (size_t i = 0; i < pats.size(); ++i) {
+        if (used && !(*used)[i]) continue;
+        const Pattern &p = pats[i];
+        if (!p0) {
+            p0 = &p;
+            continue;
+        }
+        if (p.n_in != p0->n_in || p.n_out != p0->n_out) return false;
         for (int o = 0; o < p.n_out; ++o)
-            if (p.out_mode[o] != p0.out_mode[o]) return false;
+            if (p.out_mode[o] != p0->out_mode[o]) return false;
     }
+    if (!p0) return false;
     int nx = 0;
-    for (int o = 0; o < p0.n_out; ++o) nx += p0.out_mode[o] == kModeXor;
+    for (int o = 0; o < p0->n_out; ++o) nx += p0->out_mode[o] == kModeXor;
     if (nx == 0) *acc = kAccNone;
-    else if (nx == p0.n_out) *acc = kAccAll;
-    else if (nx == p0.n_out - 1 && p0.out_mode[p0.n_out - 1] == kModeWrite) *acc = kAccAllButLast;
+    else if (nx == p0->n_out) *acc = kAccAll;
+    else if (nx == p0->n_out - 1 && p0->out_mode[p0->n_out - 1] == kModeWrite) *acc = kAccAllButLast;
     else return false;
-    *n = p0.n_in;
-    *l = p0.n_out;
+    *n = p0->n_in;
+    *l = p0->n_out;
     return true;
 }
 
@@ -239,7 +219,7 @@ struct Streams {
 // One launch over a tile source (plan or implicit region) with a pattern set.
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
-                       uint64_t implicit_len, hipStream_t stream);
+                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used);
 
 // ============================================================== plans
 // Tiles of one extent end on 4 KiB boundaries of the arena offset, so interior
@@ -275,10 +255,23 @@ struct cec_plan {
     uint64_t total = 0;
     bool overlap = false;
     int64_t n_line_tiles = 0;   // full kTile tiles at a 128-B aligned arena offset
-    Tile *d_tiles = nullptr;
+    Tile *d_tiles = nullptr;    // from dev_cache() (owned plans only; views borrow)
+    bool owned = false;
     std::vector<cec_extent> h_ext;  // validation of per-op pattern indices
     std::vector<Tile> h_tiles;      // kept alive for the async upload
+    mutable Tracker uses;           // the streams of the tile upload and of every launch
 };
+
+CEC_API int cec_plan_destroy(cec_plan *p) {
+    if (!p) return CEC_OK;
+    int rc = CEC_OK;
+    // only this plan's own work: its upload and its launches on every stream used
+    if (hipError_t e = p->uses.wait(p->device); e != hipSuccess)
+        rc = fail(CEC_EHIP, "cec_plan_destroy: a launch of this plan failed: %s", hipGetErrorString(e));
+    if (p->owned) dev_cache().release(p->device, p->d_tiles, sizeof(Tile) * p->n_tiles);
+    delete p;
+    return rc;
+}
 
 CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *stream) {
     if (!out || n < 0 || (n > 0 && !ext)) return fail(CEC_EINVAL, "cec_plan_create: bad args");
@@ -315,28 +308,22 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
     }
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (p->n_tiles > 0) {
-        if (hipMalloc(&p->d_tiles, sizeof(Tile) * p->n_tiles) != hipSuccess) {
+        const size_t bytes = sizeof(Tile) * p->n_tiles;
+        p->d_tiles = static_cast<Tile *>(dev_cache().acquire(dev, bytes));
+        if (!p->d_tiles) {
             delete p;
-            return fail(CEC_ENOMEM, "cec_plan_create: hipMalloc tiles");
+            return fail(CEC_ENOMEM, "cec_plan_create: %zu bytes of tiles", bytes);
         }
-        if (hipMemcpyAsync(p->d_tiles, p->h_tiles.data(), sizeof(Tile) * p->n_tiles,
-                           hipMemcpyHostToDevice, s) != hipSuccess) {
-            (void)hipFree(p->d_tiles);
-            delete p;
+        p->owned = true;
+        if (hipMemcpyAsync(p->d_tiles, p->h_tiles.data(), bytes, hipMemcpyHostToDevice, s) != hipSuccess) {
+            (void)hipGetLastError();
+            cec_plan_destroy(p);
             return fail(CEC_EHIP, "cec_plan_create: tile upload failed");
         }
+        p->uses.note(s);  // destroy waits for the upload too
     }
     *out = p;
     return CEC_OK;
-}
-
-CEC_API int cec_plan_destroy(cec_plan *p) {
-    if (!p) return CEC_OK;
-    int rc = CEC_OK;
-    if (hipDeviceSynchronize() != hipSuccess) rc = fail(CEC_EHIP, "hipDeviceSynchronize");
-    if (p->d_tiles) (void)hipFree(p->d_tiles);
-    delete p;
-    return rc;
 }
 
 CEC_API int cec_plan_num_extents(const cec_plan *p) { return p ? p->n_ext : 0; }
@@ -382,7 +369,7 @@ static size_t occupancy_lds(int dev, uint32_t split_shift) {
 
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
-                       uint64_t implicit_len, hipStream_t stream) {
+                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
     for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
@@ -398,36 +385,43 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
         if (n_tiles > 0xFFFFFFFFull) return fail(CEC_EINVAL, "region too large");
     }
     if (n_tiles == 0 || pats.empty()) return CEC_OK;
-    int nt = 1, lt = 0;
-    for (const Pattern &p : pats) {
-        nt = std::max(nt, p.n_in);
-        lt = std::max(lt, p.n_out);
+    int nt = 1, lt = 0, max_rows = 0;
+    for (size_t i = 0; i < pats.size(); ++i) {
+        if (used && !(*used)[i]) continue;
+        nt = std::max(nt, pats[i].n_in);
+        lt = std::max(lt, pats[i].n_out);
+        max_rows = std::max(max_rows, pats[i].lds_rows);
     }
     if (lt == 0) return CEC_OK;
-    const Pattern *dp = nullptr;
-    if (int r = upload_patterns(dev, pats, rows, &dp)) return r;
-    a.patterns = dp;
-    a.rows = reinterpret_cast<const uint8_t *>(dp + pats.size());
+    // Patterns and the LDS engine's product rows are uploaded as one blob: rows follow
+    // the patterns (16-B aligned: sizeof(Pattern) is a multiple of 16).
+    std::string key(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
+    key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
+    PatEntry *entry = nullptr;
+    if (int r = pattern_get(dev, std::move(key), stream, &entry)) return r;
+    a.patterns = reinterpret_cast<const Pattern *>(entry->d);
+    a.rows = entry->d + pats.size() * sizeof(Pattern);
     a.n_tiles = static_cast<uint32_t>(n_tiles);
     // One workgroup per (part of a) tile, dispatched in tile order, so the set of
     // tiles in flight is a contiguous window of the arenas (measured 5-12 % over a
     // persistent grid-stride grid: DESIGN.md).  The LDS engine stages its pattern's
     // product rows per workgroup (512 B for an RS(3,2) encode, from L2).
     const bool lds = g_engine.load() == CEC_ENGINE_LDS;
-    int max_rows = 0;
-    for (const Pattern &p : pats) max_rows = std::max(max_rows, p.lds_rows);
     a.split_shift = split_shift_for(st, plan);
     const size_t lds_bytes = std::max(lds ? static_cast<size_t>(max_rows) * 256 : 0,
                                       occupancy_lds(dev, a.split_shift));
     const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, 0x7FFFFFFFull));
     int en, el, eacc;
-    const bool exact = exact_shape(pats, &en, &el, &eacc) &&
+    const bool exact = exact_shape(pats, used, &en, &el, &eacc) &&
                        (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, lds_bytes, stream)
                             : launch_exact<PermEngine>(en, el, eacc, a, grid, lds_bytes, stream));
     if (!exact) {
         if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, lds_bytes, stream);
         else launch_generic<PermEngine>(nt, lt, a, grid, lds_bytes, stream);
     }
+    // the tables' and the plan's streams, for eviction and destroy (host-side only)
+    entry->uses.note(stream);
+    if (plan) plan->uses.note(stream);
     HIP_TRY(hipGetLastError());
     return CEC_OK;
 }
@@ -444,8 +438,11 @@ struct Combo {
     std::vector<Out> outs;  // install output (if any) is last
 };
 
+// `used`: which combos the launch's tiles name (NULL = all; a persistent pattern table
+// may hold more than one launch uses: the kernel shape is chosen from the used ones).
 static int run_combos(int dev, const Streams &st, const std::vector<Combo> &combos,
-                      const cec_plan *plan, uint64_t implicit_len, hipStream_t stream) {
+                      const cec_plan *plan, uint64_t implicit_len, hipStream_t stream,
+                      const std::vector<char> *used = nullptr) {
     size_t max_out = 0;
     for (const Combo &c : combos) max_out = std::max(max_out, c.outs.size());
     const int engine = g_engine.load();
@@ -477,7 +474,7 @@ static int run_combos(int dev, const Streams &st, const std::vector<Combo> &comb
             if (engine == CEC_ENGINE_LDS) assign_rows(p, rows);
             pats.push_back(p);
         }
-        if (int r = run_combine(dev, st, pats, rows, plan, implicit_len, stream)) return r;
+        if (int r = run_combine(dev, st, pats, rows, plan, implicit_len, stream, used)) return r;
     }
     return CEC_OK;
 }

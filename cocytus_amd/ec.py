@@ -16,7 +16,8 @@ import os
 from typing import Iterable, Sequence
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcocytus_ec.so")
+# CEC_LIB_PATH: load another build of the library (A/B measurement of two builds)
+LIB_PATH = os.environ.get("CEC_LIB_PATH") or os.path.join(HERE, "libcocytus_ec.so")
 
 CEC_OK = 0
 CEC_EINVAL = -1
@@ -68,6 +69,14 @@ class HostUpdate(ctypes.Structure):
         ("len", ctypes.c_uint32),
         ("src_lid", ctypes.c_uint32),
     ]
+
+
+class CacheInfo(ctypes.Structure):
+    """cec_cache_info: the coefficient-table cache and the idle-buffer caches."""
+
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "pattern_entries", "pattern_bytes", "pattern_uploads", "pattern_evictions",
+        "pattern_entry_limit", "device_cached_bytes", "pinned_cached_bytes")]
 
 
 _vp = ctypes.c_void_p
@@ -130,6 +139,9 @@ _SIGS = {
     "cec_recovery_pool_residual": ([_vp, _i, _vp, _vp], _i),
     "cec_recovery_pool_end": ([_vp, _i], _i),
     "cec_recovery_pool_active": ([_vp], _i),
+    "cec_cache_get_info": ([ctypes.POINTER(CacheInfo)], _i),
+    "cec_cache_set_pattern_limit": ([_i], _i),
+    "cec_cache_trim": ([], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
     "cec_event_destroy": ([_vp], _i),
     "cec_event_record": ([_vp, _vp], _i),
@@ -173,6 +185,8 @@ def lib() -> ctypes.CDLL:
         )
     L = ctypes.CDLL(LIB_PATH)
     for name, (args, res) in _SIGS.items():
+        if os.environ.get("CEC_LIB_PATH") and not hasattr(L, name):
+            continue  # an older build under A/B measurement: bind what it has
         fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = res
@@ -245,6 +259,21 @@ def set_waves_per_cu(waves: int) -> None:
 
 def get_waves_per_cu() -> int:
     return lib().cec_get_waves_per_cu()
+
+
+def cache_info() -> dict:
+    """cec_cache_get_info for the current device, as a dict."""
+    ci = CacheInfo()
+    _check(lib().cec_cache_get_info(ctypes.byref(ci)))
+    return {n: int(getattr(ci, n)) for n, _ in CacheInfo._fields_}
+
+
+def cache_set_pattern_limit(entries: int) -> None:
+    _check(lib().cec_cache_set_pattern_limit(entries))
+
+
+def cache_trim() -> None:
+    _check(lib().cec_cache_trim())
 
 
 def arena_stride(nbytes: int) -> int:

@@ -101,7 +101,11 @@ int cec_arenas_free(void *slab);
  * stream ordered after it.  Overlapping [off, off+len) ranges are recorded: RMW ops
  * (cec_diff_update, cec_apply_diffs) refuse such a plan with CEC_EOVERLAP. */
 int cec_plan_create(cec_plan **out, const cec_extent *extents, int n, void *stream);
-int cec_plan_destroy(cec_plan *plan);           /* synchronises with pending work */
+/* Waits for the streams the plan was used on (its upload and launches; an event
+ * recorded on each), never for the device or other streams.  Destroy plans (and
+ * sessions, drainers, pools) before the streams they were used on.  A plan used inside
+ * a captured graph must outlive the graph's replays. */
+int cec_plan_destroy(cec_plan *plan);
 int cec_plan_num_extents(const cec_plan *plan);
 int64_t cec_plan_num_tiles(const cec_plan *plan);
 uint64_t cec_plan_total_bytes(const cec_plan *plan); /* sum of extent lengths */
@@ -210,7 +214,11 @@ uint8_t *cec_drainer_staging(cec_drainer *d, size_t *capacity);
  * the arenas, participants `mask` (start_recovery, memcached.c:8136-8151).  The
  * residual lives in HBM.  Peer data, diffs and the other parities' residuals may be
  * host memory (pageable or pinned: staged through a pipelined pinned uploader) or
- * device memory (used in place).  All calls are synchronous. */
+ * device memory (used in place).  All calls are synchronous: their results (device,
+ * pinned or pageable) are complete on return and the caller may reuse its buffers.
+ * destroy waits only for the streams the session's calls used; work the CALLER queued
+ * on cec_recovery_residual(r) (e.g. shipping it with cec_copy on another stream) must
+ * be complete before destroy, since the residual's memory is then reused. */
 typedef struct cec_recovery cec_recovery;
 
 int cec_recovery_create(cec_recovery **out, int k, int m, const int *matrix, int lid_self,
@@ -298,6 +306,28 @@ int cec_recovery_pool_residual(cec_recovery_pool *pool, int id, void *dst, void 
 /* recovery_req_remove: release the request's units. */
 int cec_recovery_pool_end(cec_recovery_pool *pool, int id);
 int cec_recovery_pool_active(const cec_recovery_pool *pool);
+
+/* ---- process-wide caches ----
+ * Coefficient tables are uploaded once per distinct content (asynchronously, on a
+ * library stream the caller's stream then waits on) and kept in an LRU cache of at
+ * most pattern_entry_limit entries per device; tables used inside a stream capture
+ * stay for the life of the process (the graph holds their address).  Idle device and
+ * pinned buffers of plans, recovery sessions, drainers and pools are kept for reuse
+ * (freeing them would wait for the whole device), capped at 2 GiB / 1 GiB. */
+typedef struct cec_cache_info {
+    uint64_t pattern_entries;      /* coefficient-table sets cached on this device */
+    uint64_t pattern_bytes;        /* their device bytes (a pinned mirror each as well) */
+    uint64_t pattern_uploads;      /* sets uploaded since start (misses) */
+    uint64_t pattern_evictions;    /* LRU evictions since start */
+    uint64_t pattern_entry_limit;
+    uint64_t device_cached_bytes;  /* idle device buffers held for reuse (all devices) */
+    uint64_t pinned_cached_bytes;  /* idle pinned host buffers held for reuse */
+} cec_cache_info;
+int cec_cache_get_info(cec_cache_info *out);       /* current device */
+int cec_cache_set_pattern_limit(int entries);      /* default 4096 (CEC_PATTERN_CACHE_ENTRIES) */
+/* Free every idle cached buffer and every coefficient-table set not used by a captured
+ * graph (waits for their last uses only). */
+int cec_cache_trim(void);
 
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
 int cec_event_create(void **ev);

@@ -85,11 +85,34 @@ typedef struct {
     pthread_barrier_t *bar;
 } bench_arg;
 
+/* splitmix64 bytes [lo, hi) of the stream seeded `seed` (8-byte words; word w is
+ * the w+1-th output), the synthetic input of SURVEY §8d. */
+static void fill_splitmix(uint8_t *buf, uint64_t seed, size_t lo, size_t hi)
+{
+    for (size_t i = lo & ~(size_t)7; i < hi; i += 8) {
+        uint64_t z = seed + (uint64_t)(i / 8 + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        if (i >= lo && i + 8 <= hi) {
+            memcpy(buf + i, &z, 8);
+            continue;
+        }
+        for (int b = 0; b < 8; ++b)
+            if (i + (size_t)b >= lo && i + (size_t)b < hi) buf[i + (size_t)b] = (uint8_t)(z >> (8 * b));
+    }
+}
+
 static void *bench_worker(void *p)
 {
     bench_arg *a = (bench_arg *)p;
     const int k = a->k, m = a->m;
     const long n = a->n;
+    /* each thread fills and first-touches its own stripes (NUMA-local pages on a
+     * multi-socket host); untimed */
+    const size_t lo = (size_t)a->s0 * (size_t)n, hi = (size_t)a->s1 * (size_t)n;
+    for (int j = 0; j < k; ++j) fill_splitmix(a->data[j], 0xC0C70001ull + (uint64_t)j, lo, hi);
+    for (int q = 0; q < m; ++q) memset(a->parity[q] + lo, 0, hi - lo);
     pthread_barrier_wait(a->bar);
     for (int r = 0; r < a->reps; ++r) {
         for (long s = a->s0; s < a->s1; ++s) {
@@ -121,17 +144,8 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
     int *matrix = ref_big_vandermonde(k + m, k);
     uint8_t *data[32], *parity[32];
     const size_t bytes = (size_t)n * (size_t)nstripes;
-    for (int j = 0; j < k; ++j) {
-        data[j] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
-        uint64_t x = 0xC0C70001ull + (uint64_t)j;
-        for (size_t i = 0; i < bytes; i += 8) {   /* splitmix64 fill */
-            uint64_t z = (x += 0x9E3779B97F4A7C15ull);
-            z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-            z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-            z ^= z >> 31;
-            memcpy(data[j] + i, &z, (bytes - i) < 8 ? (bytes - i) : 8);
-        }
-    }
+    /* filled by the workers, each its own stripes (bench_worker) */
+    for (int j = 0; j < k; ++j) data[j] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
     for (int q = 0; q < m; ++q) parity[q] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
     pthread_barrier_t bar;
     pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
@@ -148,8 +162,8 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
         pthread_create(&tid[t], NULL, bench_worker, a);
     }
     struct timespec t0, t1;
+    pthread_barrier_wait(&bar);  /* every worker has filled its stripes */
     clock_gettime(CLOCK_MONOTONIC, &t0);
-    pthread_barrier_wait(&bar);
     for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     for (int t = 0; t < threads; ++t) { free(args[t].out); free(args[t].res); }

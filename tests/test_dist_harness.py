@@ -72,6 +72,90 @@ def test_layouts():
     assert bench.layout("rs32_mixed") == (s, arena)  # seeded
 
 
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_bench(args, env_extra=None, timeout=300):
+    import subprocess
+    import sys
+
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_self_launches_ranks(world):
+    """`python bench.py --gpus N` with no torch.distributed.run parent (how the driver runs
+    it) starts N ranks itself and prints exactly ONE JSON line on stdout (rank 0's), with
+    n_gpus = N, contiguous shards and the max over ranks (gloo, no GPU)."""
+    import json
+
+    r = _run_bench(["--gpus", str(world), "--harness-check"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == world and out["gpus_arg"] == world
+    per = 65536
+    assert sorted(tuple(s) for s in out["shards"]) == [(q, q * per, (q + 1) * per) for q in range(world)]
+    assert out["max_rank"] == world - 1  # the slowest rank's numbers are the ones reported
+    assert out["slowest_sleep"] == pytest.approx(0.01 * world)
+    assert out["elapsed_max"] >= 0.01 * world
+
+
+def test_bench_single_rank_runs_in_process():
+    import json
+
+    r = _run_bench(["--harness-check"])
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["n_gpus"] == 1 and out["shards"] == [[0, 0, 65536]]
+
+
+def test_bench_world_size_mismatch_refused():
+    r = _run_bench(["--gpus", "2", "--harness-check"],
+                   env_extra={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=3" in r.stderr
+
+
+def test_bench_backend_auto():
+    import bench
+
+    old = os.environ.pop("CEC_BENCH_DEVICE", None)
+    try:
+        assert bench.parse([]).dist_backend == "nccl"
+        os.environ["CEC_BENCH_DEVICE"] = "0"  # every rank on one card: RCCL refuses, gloo
+        assert bench.parse([]).dist_backend == "gloo"
+        assert bench.parse(["--dist-backend", "nccl"]).dist_backend == "nccl"
+    finally:
+        os.environ.pop("CEC_BENCH_DEVICE", None)
+        if old is not None:
+            os.environ["CEC_BENCH_DEVICE"] = old
+
+
+def test_cpu_thread_sweep():
+    import bench
+
+    assert bench.cpu_thread_counts(256) == [1, 16, 64, 256]
+    assert bench.cpu_thread_counts(8) == [1, 8]
+    assert bench.cpu_thread_counts(1) == [1]
+    assert bench.cpu_thread_counts(64) == [1, 16, 64]
+
+
+def test_cpu_baseline_small():
+    """The CPU-baseline leg (oracle, AVX2 restatement) on a short sweep: both the
+    1-thread reference configuration and the all-thread ceiling, cores stated."""
+    import bench
+
+    cb = bench.cpu_baseline(3, 2, 4096, 0.4, threads_list=[1, 2])
+    assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
+    assert cb["reference_config"]["threads"] == 1 and cb["reference_config"]["value"] > 0
+    assert [p["threads"] for p in cb["sweep"]] == [1, 2]
+
+
 def test_bench_arguments():
     """The driver's contract: no flags = N=1, the metric's workload, steps/warmup that
     finish in minutes; the other device-resident configs ride along (--also)."""
@@ -80,7 +164,7 @@ def test_bench_arguments():
     a = bench.parse([])
     assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "perm")
     assert 1 <= a.steps <= 100 and a.warmup >= 1
-    assert set(a.also.split(",")) == {"rs32_mixed", "rs32_1m", "rs42_64k"}
+    assert set(a.also.split(",")) == {"rs32_mixed", "rs32_1m", "rs42_64k", "rs32_diff_update", "rs32_e2e"}
     assert bench.parse(["--also="]).also == ""
     with pytest.raises(SystemExit):
         bench.parse(["--also=rs99"])

@@ -1,0 +1,279 @@
+"""GPU: the runtime around the kernels -- completion tracking, caches, capture.
+
+* destroy of a plan / drainer / recovery session / recovery pool waits for that
+  object's own work only, never for unrelated work on another stream;
+* cec_recovery_solve / _finish are synchronous (cocytus_ec.h): a pinned output is
+  complete when the call returns, with no device synchronisation by the caller;
+* the coefficient-table cache is bounded (LRU) and the idle recoverer's pool does not
+  mint new cache keys per flush: device memory stays flat over 10^5 random flushes;
+* a graph capture works on a cold cache (tables never seen before), no warm-up call.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def busy(gpu):
+    """launch(): queue ~0.5 s of unrelated GPU work on a fresh stream; returns its event."""
+    torch, _ = gpu
+    t0 = time.perf_counter()
+    torch.cuda._sleep(10_000_000)
+    torch.cuda.synchronize()
+    per_cycle = (time.perf_counter() - t0) / 10_000_000
+    cycles = int(min(max(0.5 / max(per_cycle, 1e-12), 1e6), 5e10))
+
+    def launch():
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(cycles)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        return ev
+
+    return launch
+
+
+def _rs32(torch, ec, B=256, n=4096):
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(11)
+    data = [torch.randint(0, 256, (B * n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    return k, m, mat, data, parity
+
+
+def test_plan_destroy_ignores_other_streams(gpu, busy):
+    torch, ec = gpu
+    k, m, mat, data, parity = _rs32(torch, ec)
+    s = torch.cuda.Stream()
+    plan = ec.Plan([(i * 4096, 0, 4096, 0) for i in range(256)], stream=s)
+    ec.encode(k, m, mat, data, parity, plan, s)
+    s.synchronize()  # the plan's own work is complete
+    other = busy()
+    t0 = time.perf_counter()
+    plan.destroy()
+    dt = time.perf_counter() - t0
+    still_busy = not other.query()
+    torch.cuda.synchronize()
+    assert still_busy, f"plan destroy waited for another stream's work ({dt * 1e3:.1f} ms)"
+
+
+def test_plan_destroy_waits_for_own_launch(gpu, busy):
+    """The plan's tiles stay valid until its last launch completed, on any stream."""
+    torch, ec = gpu
+    k, m, mat, data, parity = _rs32(torch, ec)
+    s = torch.cuda.Stream()
+    ev = busy()
+    s.wait_event(ev)  # the plan's launch is queued behind 0.5 s of work
+    plan = ec.Plan([(i * 4096, 0, 4096, 0) for i in range(256)], stream=s)
+    ec.encode(k, m, mat, data, parity, plan, s)
+    plan.destroy()
+    assert ev.query(), "destroy returned before the plan's own launch ran"
+    torch.cuda.synchronize()
+    from oracle import pyoracle
+
+    host = [d[:4096].cpu().numpy() for d in data]
+    exp = pyoracle.encode(mat, k, m, host)
+    assert all(np.array_equal(parity[p][:4096].cpu().numpy(), exp[p]) for p in range(m))
+
+
+def test_drainer_destroy_ignores_other_streams(gpu, busy):
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    parity = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    diffs = [np.full(4096, i + 1, np.uint8) for i in range(8)]
+    d = ec.Drainer(k, m, mat, k, staging_bytes=1 << 20)
+    d.apply([(diffs[i], i * 4096, i % k) for i in range(8)], parity)
+    other = busy()
+    d.destroy()
+    still_busy = not other.query()
+    torch.cuda.synchronize()
+    assert still_busy, "drainer destroy waited for another stream's work"
+
+
+def test_recovery_and_pool_destroy_ignore_other_streams(gpu, busy):
+    torch, ec = gpu
+    k, m, mat, data, parity = _rs32(torch, ec, B=16)
+    ec.encode_region(k, m, mat, data, parity, 16 * 4096)
+    torch.cuda.synchronize()
+    mask = ec.recovery_mask(k, m, k, [0, 1, 1, 1, 1])
+    r = ec.Recovery(k, m, mat, k, mask, 0, 15, parity[0])
+    r.add_peer(1, data[1])
+    pool = ec.RecoveryPool(k, m, mat, k, parity[0], capacity_units=64)
+    rid = pool.begin(mask, 3, 3)
+    pool.add_peer(rid, 1, data[1][3 * 4096:4 * 4096].cpu().numpy())
+    pool.flush()
+    other = busy()
+    r.destroy()
+    pool.destroy()
+    still_busy = not other.query()
+    torch.cuda.synchronize()
+    assert still_busy, "session / pool destroy waited for another stream's work"
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_recovery_solve_is_synchronous_on_pinned_output(gpu, oracle, fused):
+    """with device survivors and a pinned output, the rebuilt bytes
+    must be in the output when finish / solve return -- read with no device sync."""
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    n_units = 4096  # 16 MiB: long enough that an async return would be caught
+    n = n_units * 4096
+    g = torch.Generator(device="cuda").manual_seed(5)
+    data = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, parity, n)
+    want = data[0].cpu().numpy()
+    mask = ec.recovery_mask(k, m, k, [0, 1, 1, 1, 1])  # D0 lost, leader P0
+    s = torch.cuda.Stream()
+    for attempt in range(3):
+        out = torch.zeros(n, dtype=torch.uint8).pin_memory()
+        torch.cuda.synchronize()
+        with ec.Recovery(k, m, mat, k, mask, 0, n_units - 1, parity[0]) as rec:
+            rec.add_peer(1, data[1], stream=s)
+            if fused:
+                rec.finish(2, data[2], {}, {0: out}, stream=s)
+            else:
+                rec.add_peer(2, data[2], stream=s)
+                rec.solve({}, {0: out}, stream=s)
+            got = out.numpy().copy()  # no synchronize: the call is synchronous
+        assert np.array_equal(got, want), f"attempt {attempt}: output incomplete on return"
+
+
+def test_pattern_cache_lru_bound(gpu, oracle):
+    """More distinct coefficient sets than the limit: entries stay at the limit, evicted
+    tables are re-uploaded on reuse, and every result stays bit-exact."""
+    torch, ec = gpu
+    n = 8192
+    src = oracle.splitmix_bytes(3, n)
+    ds = torch.from_numpy(src).cuda()
+    ec.cache_set_pattern_limit(16)
+    try:
+        before = ec.cache_info()
+        for rep in range(2):
+            for c in range(2, 66):  # 64 distinct sets, 4x the limit
+                dd = torch.zeros(n, dtype=torch.uint8, device="cuda")
+                ec.region_multiply(ds, c, n, dd, 1)
+                torch.cuda.synchronize()
+                exp = np.zeros(n, np.uint8)
+                oracle.region_multiply(src, c, exp, 1)
+                assert np.array_equal(dd.cpu().numpy(), exp), (rep, c)
+                assert ec.cache_info()["pattern_entries"] <= 16
+        after = ec.cache_info()
+        assert after["pattern_evictions"] - before["pattern_evictions"] >= 100
+    finally:
+        ec.cache_set_pattern_limit(4096)
+
+
+def test_pool_flushes_keep_memory_flat(gpu, oracle):
+    """10^5 randomized idle-recoverer flushes (random peer order, partial replies,
+    leader solve or not): the coefficient-table cache gains at most the pool's pattern
+    table versions (bounded by the distinct (peer set, touch, lost) keys, not by the
+    request mix), and device memory in use does not grow."""
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    units = 512
+    n = units * 4096
+    g = torch.Generator(device="cuda").manual_seed(9)
+    data = [torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, parity, n)
+    hostd = [d.cpu().numpy() for d in data]
+    out = [torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    rng = np.random.default_rng(1)
+    masks = {j: ec.recovery_mask(k, m, k, [int(i != j) for i in range(k + m)]) for j in range(k)}
+    pool = ec.RecoveryPool(k, m, mat, k, parity[0], capacity_units=128)
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info()[0]
+    info0 = ec.cache_info()
+    flushes = 0
+    checked = 0
+    while flushes < 100_000:
+        live = []
+        for _ in range(int(rng.integers(1, 6))):
+            lost = int(rng.integers(0, k))
+            u = int(rng.integers(0, units))
+            rid = pool.begin(masks[lost], u, u)
+            peers = [j for j in range(k) if j != lost]
+            rng.shuffle(peers)
+            live.append((rid, lost, u, peers, int(rng.integers(1, 3))))
+        # replies arrive in random order, some requests get only one of two this flush
+        for rid, lost, u, peers, first in live:
+            for j in peers[:first]:
+                pool.add_peer(rid, j, hostd[j][u * 4096:(u + 1) * 4096])
+        if rng.integers(0, 2):
+            pool.flush_solve(out)
+        else:
+            pool.flush()
+        flushes += 1
+        for rid, lost, u, peers, first in live:
+            for j in peers[first:]:
+                pool.add_peer(rid, j, hostd[j][u * 4096:(u + 1) * 4096])
+        solved = pool.flush_solve(out)
+        flushes += 1
+        del solved
+        if flushes % 20_000 < 2:  # spot-check the rebuilt units against the originals
+            torch.cuda.synchronize()
+            for rid, lost, u, peers, first in live:
+                got = out[lost][u * 4096:(u + 1) * 4096].cpu().numpy()
+                assert np.array_equal(got, hostd[lost][u * 4096:(u + 1) * 4096]), (flushes, lost, u)
+                checked += 1
+        for rid, *_ in live:
+            pool.end(rid)
+    torch.cuda.synchronize()
+    info1 = ec.cache_info()
+    free1 = torch.cuda.mem_get_info()[0]
+    pool.destroy()
+    assert checked > 0
+    # pattern keys: (2^k peer sets) x (touch) x (lost + 1) bounds the table versions
+    assert info1["pattern_entries"] - info0["pattern_entries"] <= 2 ** k * 2 * (k + 1)
+    assert info1["pattern_entries"] <= info1["pattern_entry_limit"]
+    assert free0 - free1 < (64 << 20), f"device memory grew by {(free0 - free1) >> 20} MiB"
+
+
+def test_graph_capture_cold_cache(gpu, oracle):
+    """Capture an RS(5,3) encode + double-erasure decode whose coefficient tables were
+    never used before (cold cache, no warm-up call), replay, compare with the oracle;
+    then trim the caches: the captured tables survive, and the graph still replays."""
+    torch, ec = gpu
+    k, m, n, B = 5, 3, 4096, 64
+    mat = ec.coding_matrix(k, m)
+    host = [oracle.splitmix_bytes(0xC0C70010 + j, B * n) for j in range(k)]
+    data = [torch.from_numpy(h).cuda() for h in host]
+    parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    out = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(k)]
+    mask = sum(1 << x for x in (1, 2, 4, 5, 6))  # D0, D3 lost; parities P5, P6 (lids 5, 6)
+    ep = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
+    dp = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        s = torch.cuda.current_stream()
+        ec.encode(k, m, mat, data, parity, ep, s)
+        ec.decode(k, m, mat, [mask], data + parity, out, dp, s)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, host)
+    for p in range(m):
+        assert np.array_equal(parity[p].cpu().numpy(), exp[p])
+    assert torch.equal(out[0], data[0]) and torch.equal(out[3], data[3])
+    ec.cache_trim()  # captured tables are kept: the graph still holds their address
+    for t in parity + out:
+        t.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    for p in range(m):
+        assert np.array_equal(parity[p].cpu().numpy(), exp[p])
+    assert torch.equal(out[0], data[0]) and torch.equal(out[3], data[3])
+    ep.destroy()
+    dp.destroy()
