@@ -219,14 +219,15 @@ def cpu_baseline(k, m, n, wall_s, threads_list=None):
     }
 
 
-def load_traffic(workload):
-    """HBM bytes per launch from the committed rocprofv3 --pmc summary (profiles/)."""
+def load_traffic(workload, ops=("encode", "decode")):
+    """HBM bytes per launch of each op from the committed rocprofv3 --pmc summary
+    (profiles/pmc_traffic.json, written by tools/profile_round.sh)."""
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             e = json.load(f).get(workload, {})
-        return e.get("encode_hbm_bytes_per_launch"), e.get("decode_hbm_bytes_per_launch")
+        return tuple(e.get(f"{op}_hbm_bytes_per_launch") for op in ops)
     except (OSError, ValueError):
-        return None, None
+        return tuple(None for _ in ops)
 
 
 def setup(backend="nccl"):
@@ -403,7 +404,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
                      "frac": round(gbps / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": nbytes,
                      "launch_ms": round(ms, 4),
                      "kernel": "combine_kernel<2,3,*,kAccAllButLast,exact> (cec_diff_update, install)",
-                     "traffic": load_traffic("rs32_diff_update")[0]},
+                     "traffic": load_traffic("rs32_diff_update", ("diff_update",))[0]},
         "verified": bool(ok and bad == 0.0),
     }
 

@@ -277,3 +277,36 @@ def test_graph_capture_cold_cache(gpu, oracle):
     assert torch.equal(out[0], data[0]) and torch.equal(out[3], data[3])
     ep.destroy()
     dp.destroy()
+
+
+def test_graph_capture_on_the_warm_stream(gpu, oracle):
+    """The tables were first uploaded on stream s (their upload event recorded there) and
+    the capture then runs on that same stream: no event call may touch it while it
+    captures.  Replays are bit-exact; direct launches afterwards still work."""
+    torch, ec = gpu
+    k, m, n, B = 4, 3, 4096, 32  # a code no other test uses: a fresh upload on s
+    mat = ec.coding_matrix(k, m)
+    host = [oracle.splitmix_bytes(0xC0C70020 + j, B * n) for j in range(k)]
+    data = [torch.from_numpy(h).cuda() for h in host]
+    parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    side = torch.cuda.Stream()
+    plan = ec.Plan([(i * n, 0, n, 0) for i in range(B)], stream=side)
+    ec.encode(k, m, mat, data, parity, plan, side)  # upload queued on `side`, not waited for
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=side):
+        ec.encode(k, m, mat, data, parity, plan, side)
+    for t in parity:
+        t.zero_()
+    torch.cuda.synchronize()
+    g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, host)
+    for p in range(m):
+        assert np.array_equal(parity[p].cpu().numpy(), exp[p])
+    for t in parity:
+        t.zero_()
+    ec.encode(k, m, mat, data, parity, plan, side)
+    side.synchronize()
+    for p in range(m):
+        assert np.array_equal(parity[p].cpu().numpy(), exp[p])
+    plan.destroy()

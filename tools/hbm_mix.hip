@@ -52,6 +52,48 @@ __global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
     }
 }
 
+// The access shapes of the ops whose streams are not independent arenas:
+//   kind 0: diff-update + install, 4 reads / 3 writes, 3 of them read-modify-write
+//           (D_j, P0, P1 read then written; staging read): r0 = D, r1 = staging,
+//           r2 = P0, r3 = P1; writes go back to r0, r2, r3
+//   kind 1: the same without install (4 reads, P0 / P1 written back)
+//   kind 2: RS(3,2) decode with the lost shard rotating per 4 KiB stripe and the leader
+//           every 3 stripes (the bench): reads the 2 surviving data arenas (r0..r2) and
+//           parity r3 / r4, writes out arena w[lost]
+//   kind 3: RS(4,2) decode, 64 KiB stripes (16 tiles), lost shard rotating per stripe:
+//           reads 3 data (r0..r3) + parity r4 / r5, writes w[lost]
+//   kind 4: kind 2 with a fixed lost shard (D0) and leader (P0)
+template <int KIND>
+__global__ __launch_bounds__(256) void k_shape(Ptrs p, uint8_t *const *all, uint32_t tile_shift) {
+    const uint64_t off = (uint64_t)blockIdx.x * blockDim.x * 16 + threadIdx.x * 16;
+    const uint32_t t = blockIdx.x >> tile_shift;  // 4 KiB tile index
+    u32x4 acc = {0, 0, 0, 0};
+    auto ld = [&](const uint8_t *b) { return __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)b + off)); };
+    auto st = [&](uint8_t *b, u32x4 v) { __builtin_nontemporal_store(v, (GL u32x4 *)((uintptr_t)b + off)); };
+    if constexpr (KIND == 0 || KIND == 1) {
+        const u32x4 d = ld(all[0]), n = ld(all[1]);
+        u32x4 p0 = ld(all[2]), p1 = ld(all[3]);
+        const u32x4 x = d ^ n;
+        p0 ^= x;
+        p1 ^= x;
+        st(all[2], p0);
+        st(all[3], p1);
+        if constexpr (KIND == 0) st(all[0], n);
+    } else if constexpr (KIND == 2 || KIND == 4) {
+        const uint32_t lost = KIND == 4 ? 0 : t % 3, par = KIND == 4 ? 0 : (t / 3) % 2;
+        for (int j = 0; j < 3; ++j)
+            if (j != (int)lost) acc ^= ld(all[j]);
+        acc ^= ld(all[3 + par]);
+        st(all[6 + lost], acc);
+    } else {
+        const uint32_t stripe = t >> 4, lost = stripe % 4, par = (stripe / 4) % 2;
+        for (int j = 0; j < 4; ++j)
+            if (j != (int)lost) acc ^= ld(all[j]);
+        acc ^= ld(all[4 + par]);
+        st(all[6 + lost], acc);
+    }
+}
+
 // splitmix64 fill: the ceilings must be measured on random bytes like the bench's
 __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
     for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
@@ -63,7 +105,8 @@ __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
 }
 
 int main(int argc, char **argv) {
-    const uint64_t len = 256ull << 20;  // per arena
+    // per arena (HBM_MIX_MB overrides: the RS(4,2) 64 KiB bench uses 1 GiB arenas)
+    const uint64_t len = (getenv("HBM_MIX_MB") ? strtoull(getenv("HBM_MIX_MB"), nullptr, 0) : 256ull) << 20;
     // argv[1] = skew in bytes: arena i starts i * skew past a 2 MiB boundary inside one
     // allocation (0 = separate hipMalloc per arena, the default layout)
     const bool arena = argc > 1 && argv[1][0] == 'a';
@@ -125,6 +168,20 @@ int main(int argc, char **argv) {
                          {"1:1 copy", 1, 1}, {"2:1 (RMW-like)", 2, 1}, {"3:1 decode RS(3,2)", 3, 1},
                          {"3:2 encode RS(3,2)", 3, 2}, {"4:1 decode RS(4,2)", 4, 1},
                          {"4:2 encode RS(4,2)", 4, 2}, {"6:4 RS(6,4)-like", 6, 4}};
+    uint8_t **all;
+    CK(hipMalloc(&all, 10 * sizeof(uint8_t *)));
+    CK(hipMemcpy(all, bufs.data(), 10 * sizeof(uint8_t *), hipMemcpyHostToDevice));
+    uint32_t tshift = lanes == 256 ? 0 : lanes == 128 ? 1 : 2;
+    struct S {
+        const char *name;
+        int kind, r, w;
+    };
+    std::vector<S> shapes = {{"diff-update+install 4:3 (3 RMW)", 0, 4, 3},
+                             {"diff-update 4:2 (2 RMW)", 1, 4, 2},
+                             {"RS(3,2) decode, rotating 3:1", 2, 3, 1},
+                             {"RS(3,2) decode, fixed 3:1", 4, 3, 1},
+                             {"RS(4,2) 64K decode, rotating 4:1", 3, 4, 1}};
+    for (const S &sh : shapes) vs.push_back({sh.name, 100 + sh.kind, 0});
     const uint32_t grid = len / (16 * lanes);
     auto launch = [&](const V &v) {
         switch (v.r * 10 + v.w) {
@@ -138,6 +195,11 @@ int main(int argc, char **argv) {
         case 41: hipLaunchKernelGGL((k_mix<4, 1>), grid, lanes, 0, 0, p, sink); break;
         case 42: hipLaunchKernelGGL((k_mix<4, 2>), grid, lanes, 0, 0, p, sink); break;
         case 64: hipLaunchKernelGGL((k_mix<6, 4>), grid, lanes, 0, 0, p, sink); break;
+        case 1000: hipLaunchKernelGGL((k_shape<0>), grid, lanes, 0, 0, p, all, tshift); break;
+        case 1010: hipLaunchKernelGGL((k_shape<1>), grid, lanes, 0, 0, p, all, tshift); break;
+        case 1020: hipLaunchKernelGGL((k_shape<2>), grid, lanes, 0, 0, p, all, tshift); break;
+        case 1030: hipLaunchKernelGGL((k_shape<3>), grid, lanes, 0, 0, p, all, tshift); break;
+        case 1040: hipLaunchKernelGGL((k_shape<4>), grid, lanes, 0, 0, p, all, tshift); break;
         }
     };
     hipEvent_t e0, e1;
@@ -160,7 +222,12 @@ int main(int argc, char **argv) {
            (unsigned long long)(len >> 20), lanes * 16);
     for (size_t i = 0; i < vs.size(); ++i) {
         std::sort(ms[i].begin(), ms[i].end());
-        const double bytes = (double)(vs[i].r + vs[i].w) * len;
+        double bytes = (double)(vs[i].r + vs[i].w) * len;
+        if (vs[i].r >= 100) {  // access shapes: bytes per op
+            const int kind = vs[i].r - 100;
+            const int rw[5] = {7, 6, 4, 5, 4};
+            bytes = (double)rw[kind] * len;
+        }
         printf("%-24s median %.4f ms -> %.0f GB/s (best %.0f)\n", vs[i].name, ms[i][rounds / 2],
                bytes / (ms[i][rounds / 2] * 1e6), bytes / (ms[i][0] * 1e6));
     }

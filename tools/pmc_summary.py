@@ -27,8 +27,11 @@ import bench  # noqa: E402  (layout() of the mixed workload; no torch at import)
 
 _MIXED = sum(n for _, n in bench.layout("rs32_mixed")[0])
 ALGO["rs32_mixed"] = ((3 + 2) * _MIXED, (3 + 1) * _MIXED)
+# the fused diff-update + install (a4): read old, new, 2 parities; write 2 parities + D
+ALGO["rs32_diff_update"] = ((2 + 2 * 2 + 1) * 4096 * 65536, None)
 SHAPES = {"rs32_4k": ("<3, 2,", "<3, 1,"), "rs42_64k": ("<4, 2,", "<4, 1,"), "rs32_1m": ("<3, 2,", "<3, 1,"),
-          "rs32_mixed": ("<3, 2,", "<3, 1,")}
+          "rs32_mixed": ("<3, 2,", "<3, 1,"), "rs32_diff_update": ("<2, 3,", None)}
+OPS = {"rs32_diff_update": ("diff_update", None)}  # op names of (first, second) shape
 
 
 def one(path_glob):
@@ -53,7 +56,13 @@ def main(out, rnd):
             name = r["Name"]
             if "combine_kernel" not in name:
                 continue
-            op = "encode" if enc_key in name else "decode" if dec_key in name else name
+            ops = OPS.get(w, ("encode", "decode"))
+            if enc_key in name:
+                op = ops[0]
+            elif dec_key and dec_key in name:
+                op = ops[1]
+            else:
+                continue  # set-up kernels of the run (e.g. the diff-update's initial encode)
             res[op] = {"kernel": name, "calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
         for counter, kind in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
             cc = one(f"{out}/{kind}_{w}/**/run_counter_collection.csv")
@@ -64,16 +73,23 @@ def main(out, rnd):
                 name = r.get("Kernel_Name", "")
                 if "combine_kernel" not in name or r.get("Counter_Name") != counter:
                     continue
-                op = "encode" if enc_key in name else "decode" if dec_key in name else name
+                ops = OPS.get(w, ("encode", "decode"))
+                if enc_key in name:
+                    op = ops[0]
+                elif dec_key and dec_key in name:
+                    op = ops[1]
+                else:
+                    continue
                 acc.setdefault(op, {})
                 d = r.get("Dispatch_Id", r.get("Correlation_Id"))
                 acc[op][d] = acc[op].get(d, 0.0) + float(r["Counter_Value"])
             for op, per in acc.items():
                 vals = list(per.values())
                 res.setdefault(op, {})[counter + "_KiB_raw"] = sum(vals) / len(vals)
-        for op, algo in (("encode", ALGO[w][0]), ("decode", ALGO[w][1])):
-            e = res.get(op)
-            if not e or "avg_ns" not in e:
+        ops = OPS.get(w, ("encode", "decode"))
+        for op, algo in ((ops[0], ALGO[w][0]), (ops[1], ALGO[w][1])):
+            e = res.get(op) if op else None
+            if not e or "avg_ns" not in e or algo is None:
                 continue
             e["algorithmic_bytes"] = algo
             e["achieved_GBps"] = algo / e["avg_ns"]
@@ -86,8 +102,8 @@ def main(out, rnd):
                 e["hbm_bytes"] = rd + wr
                 e["traffic_over_algorithmic"] = (rd + wr) / algo
         summary[w] = res
-        traffic[w] = {f"{op}_hbm_bytes_per_launch": res[op].get("hbm_bytes") for op in ("encode", "decode") if op in res}
-        for op in ("encode", "decode"):
+        traffic[w] = {f"{op}_hbm_bytes_per_launch": res[op].get("hbm_bytes") for op in ops if op and op in res}
+        for op in [o for o in ops if o]:
             e = res.get(op, {})
             if "avg_ns" in e:
                 lines.append(f"| {w} | {op} | {e['avg_ns'] / 1e3:.1f} | {e['achieved_GBps']:.0f} | "
@@ -100,7 +116,8 @@ def main(out, rnd):
     with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     md = [f"# rocprofv3 summary ({rnd})", "",
-          "bench.py --steps 10 --warmup 2 per workload; durations from --kernel-trace --stats;",
+          "bench.py --steps 10 --warmup 2 per workload (rs32_diff_update: --also=rs32_diff_update, only its",
+          "<2, 3, ..., 2> kernel counted); durations from --kernel-trace --stats;",
           "HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB, gfx950 correction), separate --pmc passes.", "",
           "| workload | op | avg us | algorithmic GB/s | frac of 8 TB/s | HBM MiB/launch (PMC) | algorithmic MiB | PMC/algo |",
           "|---|---|---|---|---|---|---|---|", *lines, ""]

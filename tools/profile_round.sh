@@ -9,14 +9,15 @@ ROUND=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
 OUT=$R/gpurun_out/prof_$ROUND
 mkdir -p "$OUT"
-ARGS="--steps 10 --warmup 2 --no-cpu-baseline --also="
 cd /tmp && export TMPDIR=/tmp
-for W in ${PROF_WORKLOADS:-rs32_4k rs32_mixed rs42_64k rs32_1m}; do
+ARGS="--steps 10 --warmup 2 --no-cpu-baseline"
+for W in ${PROF_WORKLOADS:-rs32_4k rs32_mixed rs42_64k rs32_1m rs32_diff_update}; do
+  if [ "$W" = rs32_diff_update ]; then WA="--workload rs32_4k --also=rs32_diff_update"; else WA="--workload $W --also="; fi
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace_$W" -o run --output-format csv \
-      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_trace_$W.log" 2>&1
+      -- python3 "$R/bench.py" $ARGS $WA > "$OUT/bench_trace_$W.log" 2>&1
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch_$W" -o run --output-format csv \
-      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_fetch_$W.log" 2>&1
+      -- python3 "$R/bench.py" $ARGS $WA > "$OUT/bench_fetch_$W.log" 2>&1
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write_$W" -o run --output-format csv \
-      -- python3 "$R/bench.py" $ARGS --workload $W > "$OUT/bench_write_$W.log" 2>&1
+      -- python3 "$R/bench.py" $ARGS $WA > "$OUT/bench_write_$W.log" 2>&1
 done
 python3 "$R/tools/pmc_summary.py" "$OUT" "$ROUND"
