@@ -941,6 +941,31 @@ CEC_API int cec_stream_synchronize(void *stream) {
     HIP_TRY(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
     return CEC_OK;
 }
+CEC_API int cec_device_count(int *count) {
+    if (!count) return fail(CEC_EINVAL, "cec_device_count: NULL");
+    *count = 0;
+    if (hipGetDeviceCount(count) != hipSuccess) {
+        (void)hipGetLastError();
+        *count = 0;
+    }
+    return CEC_OK;
+}
+CEC_API int cec_set_device(int device) {
+    HIP_TRY(hipSetDevice(device));
+    int dev;
+    return current_device(&dev);
+}
+CEC_API int cec_stream_create(void **stream) {
+    if (!stream) return fail(CEC_EINVAL, "cec_stream_create: NULL");
+    hipStream_t s;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *stream = s;
+    return CEC_OK;
+}
+CEC_API int cec_stream_destroy(void *stream) {
+    HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
 CEC_API int cec_copy(void *dst, const void *src, size_t n, void *stream) {
     if (n && (!dst || !src)) return fail(CEC_EINVAL, "cec_copy: NULL pointer");
     int dev;

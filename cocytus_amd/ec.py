@@ -147,6 +147,10 @@ _SIGS = {
     "cec_event_record": ([_vp, _vp], _i),
     "cec_event_elapsed_ms": ([_vp, _vp, ctypes.POINTER(ctypes.c_float)], _i),
     "cec_stream_synchronize": ([_vp], _i),
+    "cec_device_count": ([ctypes.POINTER(_i)], _i),
+    "cec_set_device": ([_i], _i),
+    "cec_stream_create": ([ctypes.POINTER(_vp)], _i),
+    "cec_stream_destroy": ([_vp], _i),
     "galois_w08_region_multiply": ([_vp, _i, _i, _vp, _i], None),
     "galois_single_multiply": ([_i, _i, _i], _i),
     "galois_single_divide": ([_i, _i, _i], _i),

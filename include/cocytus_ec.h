@@ -335,6 +335,14 @@ int cec_event_destroy(void *ev);
 int cec_event_record(void *ev, void *stream);
 int cec_event_elapsed_ms(void *start, void *stop, float *ms); /* synchronises on stop */
 int cec_stream_synchronize(void *stream);
+/* Device selection for C callers (one host thread per GPU): the calling
+ * thread's current device, as hipGetDeviceCount / hipSetDevice. */
+int cec_device_count(int *count);
+int cec_set_device(int device);
+/* A non-blocking stream of the current device (each is a hardware queue: use one per
+ * thread). */
+int cec_stream_create(void **stream);
+int cec_stream_destroy(void *stream);
 /* Async copy between any host / device buffers (arena bytes to and from the server's
  * buffers); complete after cec_stream_synchronize(stream). */
 int cec_copy(void *dst, const void *src, size_t n, void *stream);

@@ -752,17 +752,25 @@ def test_registered_host_arena_zero_copy(gpu, oracle):
 def test_native_metric_harness(gpu, tmp_path):
     """tools/bench_native.c, the metric's step through the C-ABI alone (C99, no HIP
     header, no torch): 65,536 RS(3,2) stripes encoded and decoded with rotating
-    erasures; it checks every rebuilt shard against its original itself."""
+    erasures; it checks every rebuilt shard against its original itself.  Then its
+    thread-per-GPU mode with two threads pinned to this one card (CEC_NATIVE_DEVICE):
+    barrier-aligned start, max over threads, both batches verified."""
     import json
 
     exe = str(tmp_path / "bench_native")
-    subprocess.run(["gcc", "-O2", "-std=c99", "-D_POSIX_C_SOURCE=199309L", "-Wall", "-Werror",
+    subprocess.run(["gcc", "-O2", "-std=c99", "-D_POSIX_C_SOURCE=200809L", "-Wall", "-Werror", "-pthread",
                     "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tools", "bench_native.c"),
                     "-L", os.path.join(ROOT, "cocytus_amd"), "-lcocytus_ec",
                     "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd"), "-o", exe], check=True)
     r = subprocess.run([exe, "2", "1"], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stderr + r.stdout
-    assert json.loads(r.stdout)["verified"] is True
+    out = json.loads(r.stdout)
+    assert out["verified"] is True and out["n_gpus"] == 1
+    env = dict(os.environ, CEC_NATIVE_DEVICE="0")
+    r = subprocess.run([exe, "2", "1", "2"], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, r.stderr + r.stdout
+    out = json.loads(r.stdout)
+    assert out["verified"] is True and out["n_gpus"] == 2
 
 
 def test_graph_capture_replay(gpu, oracle):
