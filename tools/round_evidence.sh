@@ -1,9 +1,9 @@
 #!/bin/bash
 # tools/round_evidence.sh ROUND -- every measurement DESIGN.md quotes, on one box, one call
 # (run ON the GPU box through gpurun; build first, here: python -c 'import __graft_entry__ as g;
-# g.build()' && make -C tools).  Copy the results into profiles/r01_evidence/.  Results land in gpurun_out/evidence_ROUND/;
-# copy what is quoted into profiles/r01_evidence/ here (cp gpurun_out/evidence_ROUND/{*.jsonl,hbm_mix.txt}),
-# and run tools/pmc_summary.py on the merged gpurun_out/prof_ROUND.
+# g.build()' && make -C tools).  Results land in gpurun_out/evidence_ROUND/; copy what is
+# quoted into profiles/ROUND_evidence/ here, and run tools/pmc_summary.py on the merged
+# gpurun_out/prof_ROUND.
 set -euo pipefail
 ROUND=${1:-r01}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
@@ -28,5 +28,10 @@ timeout -k 10 200 tools/hbm_mix.bin arena random 256 >> "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
 timeout -k 10 200 tools/pool_bench.bin     > "$OUT/pool_bench.jsonl" 2>&1
 timeout -k 10 200 tools/launch_latency.bin > "$OUT/launch_latency.txt" 2>&1
+timeout -k 10 200 tools/bench_native.bin 20 3 > "$OUT/bench_native.jsonl" 2>&1
+CEC_NATIVE_DEVICE=0 timeout -k 10 200 tools/bench_native.bin 20 3 2 > "$OUT/bench_native_2threads_one_card.jsonl" 2>&1
+CEC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 > "$OUT/bench_gloo2_one_card.jsonl" 2> "$OUT/bench_gloo2.err"
+timeout -k 10 200 python tools/du_probe.py > "$OUT/du_probe.json" 2>/dev/null
+timeout -k 10 200 python tools/decode_probe.py > "$OUT/decode_probe.txt" 2>/dev/null
 [ -n "${EVID_NO_PROF:-}" ] || bash tools/profile_round.sh "$ROUND" > "$OUT/profile.log" 2>&1
 echo done > "$OUT/DONE"
