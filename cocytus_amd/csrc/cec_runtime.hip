@@ -419,9 +419,10 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
         if (lds) launch_generic<LdsEngine>(nt, lt, a, grid, lds_bytes, stream);
         else launch_generic<PermEngine>(nt, lt, a, grid, lds_bytes, stream);
     }
-    // the tables' and the plan's streams, for eviction and destroy (host-side only)
-    entry->uses.note(stream);
+    // the plan's streams, for its destroy (host-side only); the tables may be evicted
+    // again once the launch is enqueued (eviction synchronises the device)
     if (plan) plan->uses.note(stream);
+    pattern_done(entry);
     HIP_TRY(hipGetLastError());
     return CEC_OK;
 }
@@ -868,8 +869,8 @@ struct SignalCtx {  // per thread and device: a mapped pinned completion word
     int device = -1;
     uint32_t *flag = nullptr, *flag_dev = nullptr;
     uint32_t seq = 0;
-    ~SignalCtx() {
-        if (flag) (void)hipHostFree(flag);
+    ~SignalCtx() {  // (idle: every wait completed before its call returned)
+        map_cache().release(device, flag, 64);
     }
 };
 thread_local SignalCtx t_signal;
@@ -887,10 +888,10 @@ static int stream_wait(hipStream_t s) {
     HIP_TRY(hipGetDevice(&dev));
     SignalCtx &c = t_signal;
     if (c.device != dev) {
-        if (c.flag) HIP_TRY(hipHostFree(c.flag));
+        map_cache().release(c.device, c.flag, 64);
         c.flag = c.flag_dev = nullptr;
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.flag), 64,
-                              hipHostMallocMapped | hipHostMallocCoherent));
+        c.flag = static_cast<uint32_t *>(map_cache().acquire(dev, 64));
+        if (!c.flag) return fail(CEC_ENOMEM, "completion flag");
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.flag_dev), c.flag, 0));
         __atomic_store_n(c.flag, 0u, __ATOMIC_RELEASE);
         c.seq = 0;
@@ -1073,9 +1074,17 @@ struct DropInCtx {
             (void)hipStreamSynchronize(stream);
             (void)hipStreamDestroy(stream);
         }
-        if (dsrc) (void)hipFree(dsrc);
-        if (ddst) (void)hipFree(ddst);
-        if (zc) (void)hipHostFree(zc);
+        release();
+    }
+    // Buffers back to the process caches (idle: every call completed before returning);
+    // freeing them would wait for the whole device.
+    void release() {
+        dev_cache().release(device, dsrc, cap);
+        dev_cache().release(device, ddst, cap);
+        map_cache().release(device, zc, 2 * zc_cap);
+        dsrc = ddst = zc = nullptr;
+        zc_dev = nullptr;
+        cap = zc_cap = 0;
     }
 };
 thread_local DropInCtx t_ctx;
@@ -1137,14 +1146,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     if (c.device != dev) {
         if (c.stream) DROPIN_HIP(hipStreamDestroy(c.stream));
         c.stream = nullptr;
-        if (c.dsrc) DROPIN_HIP(hipFree(c.dsrc));
-        if (c.ddst) DROPIN_HIP(hipFree(c.ddst));
-        c.dsrc = c.ddst = nullptr;
-        c.cap = 0;
-        if (c.zc) DROPIN_HIP(hipHostFree(c.zc));  // device addresses are per device
-        c.zc = nullptr;
-        c.zc_dev = nullptr;
-        c.zc_cap = 0;
+        c.release();  // (device addresses of the mapped buffer are per device)
         DROPIN_HIP(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
         c.device = dev;
     }
@@ -1159,10 +1161,10 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     }
     if (n <= zero_copy_max()) {  // small pageable call: zero-copy through mapped pinned memory
         if (c.zc_cap < n) {
-            if (c.zc) DROPIN_HIP(hipHostFree(c.zc));
-            c.zc = nullptr;
+            map_cache().release(dev, c.zc, 2 * c.zc_cap);
             c.zc_cap = std::max(n, size_t(64) << 10);
-            DROPIN_HIP(hipHostMalloc(&c.zc, 2 * c.zc_cap, hipHostMallocMapped | hipHostMallocCoherent));
+            c.zc = static_cast<uint8_t *>(map_cache().acquire(dev, 2 * c.zc_cap));
+            if (!c.zc) die("galois_w08_region_multiply: mapped staging allocation failed");
             DROPIN_HIP(hipHostGetDevicePointer(&c.zc_dev, c.zc, 0));
         }
         uint8_t *zs = c.zc, *zd = c.zc + c.zc_cap;
@@ -1177,11 +1179,11 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     // larger pageable buffers: stage through device memory chunk by chunk
     const size_t want = std::min(n, kStageChunk);
     if (c.cap < want) {
-        if (c.dsrc) DROPIN_HIP(hipFree(c.dsrc));
-        if (c.ddst) DROPIN_HIP(hipFree(c.ddst));
-        c.dsrc = c.ddst = nullptr;
-        DROPIN_HIP(hipMalloc(&c.dsrc, want));
-        DROPIN_HIP(hipMalloc(&c.ddst, want));
+        dev_cache().release(dev, c.dsrc, c.cap);
+        dev_cache().release(dev, c.ddst, c.cap);
+        c.dsrc = static_cast<uint8_t *>(dev_cache().acquire(dev, want));
+        c.ddst = static_cast<uint8_t *>(dev_cache().acquire(dev, want));
+        if (!c.dsrc || !c.ddst) die("galois_w08_region_multiply: device staging allocation failed");
         c.cap = want;
     }
     for (size_t o = 0; o < n; o += kStageChunk) {

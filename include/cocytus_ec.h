@@ -308,12 +308,15 @@ int cec_recovery_pool_end(cec_recovery_pool *pool, int id);
 int cec_recovery_pool_active(const cec_recovery_pool *pool);
 
 /* ---- process-wide caches ----
- * Coefficient tables are uploaded once per distinct content (asynchronously, on a
- * library stream the caller's stream then waits on) and kept in an LRU cache of at
- * most pattern_entry_limit entries per device; tables used inside a stream capture
- * stay for the life of the process (the graph holds their address).  Idle device and
- * pinned buffers of plans, recovery sessions, drainers and pools are kept for reuse
- * (freeing them would wait for the whole device), capped at 2 GiB / 1 GiB. */
+ * Coefficient tables are uploaded once per distinct content (asynchronously, on the
+ * caller's stream; another stream waits on the upload event) and kept in an LRU cache
+ * of at most pattern_entry_limit sets per device.  Evicting synchronises the device once
+ * per batch of victims; a fixed set of codes and masks never evicts.  Tables used inside
+ * a stream capture stay for the life of the process (the graph holds their address).
+ * Idle device and pinned buffers of plans, recovery sessions, drainers, pools and the
+ * drop-in are kept for reuse (freeing them would wait for the whole device), capped at
+ * 2 GiB device / 1 GiB pinned / 512 MiB mapped pinned.  At process exit the library
+ * synchronises each device it cached state for and frees it. */
 typedef struct cec_cache_info {
     uint64_t pattern_entries;      /* coefficient-table sets cached on this device */
     uint64_t pattern_bytes;        /* their device bytes (a pinned mirror each as well) */
@@ -326,7 +329,7 @@ typedef struct cec_cache_info {
 int cec_cache_get_info(cec_cache_info *out);       /* current device */
 int cec_cache_set_pattern_limit(int entries);      /* default 4096 (CEC_PATTERN_CACHE_ENTRIES) */
 /* Free every idle cached buffer and every coefficient-table set not used by a captured
- * graph (waits for their last uses only). */
+ * graph (synchronises the current device first). */
 int cec_cache_trim(void);
 
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */

@@ -156,3 +156,21 @@ def run_dropin_daemon(tmp_path) -> str:
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, f"rc={r.returncode}\n{r.stderr[-2000:]}\n{r.stdout}"
     return r.stdout
+
+
+def run_cache_threads(tmp_path, threads=8, iters=60, limit=6) -> dict:
+    """tests/dropin/cache_threads.c: the coefficient-table cache (capped at `limit`
+    sets), the idle-buffer cache and the stream trackers under concurrent use; every
+    result checked by a round-trip property inside the program."""
+    import json
+
+    exe = os.path.join(str(tmp_path), "cache_threads")
+    subprocess.run(
+        [CC, "-O1", "-std=gnu11", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+         os.path.join(HERE, "cache_threads.c"), "-L", LIBDIR, "-lJerasure", "-lpthread",
+         f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
+        check=True,
+    )
+    r = subprocess.run([exe, str(threads), str(iters), str(limit)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, f"rc={r.returncode}\n{r.stderr[-3000:]}\n{r.stdout}"
+    return json.loads(r.stdout.strip().splitlines()[-1])

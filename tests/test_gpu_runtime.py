@@ -310,3 +310,15 @@ def test_graph_capture_on_the_warm_stream(gpu, oracle):
     for p in range(m):
         assert np.array_equal(parity[p].cpu().numpy(), exp[p])
     plan.destroy()
+
+
+def test_caches_under_concurrent_threads(gpu, tmp_path):
+    """8 host threads, a stream each, a different RS(k,m) per iteration with the table
+    cache capped at 6 sets (evicting while other threads launch), a plan per batch,
+    region multiplies, and cec_cache_trim() from one thread meanwhile: every rebuilt
+    shard and every c * (1/c) round trip exact (tests/dropin/cache_threads.c)."""
+    from tests.dropin import run_cache_threads
+
+    out = run_cache_threads(tmp_path, threads=8, iters=60, limit=6)
+    assert out["bad"] == 0 and out["errors"] == 0 and out["checks"] == 8 * 60 * 49
+    assert out["evictions"] > 0

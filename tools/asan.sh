@@ -38,7 +38,7 @@ run)
   ldd "$R/gpurun_out/dropin_daemon_asan" | grep -E "asan|Jerasure"
   timeout -k 10 60 "$R/gpurun_out/dropin_daemon_asan"
   timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
-      -k "dropin or batched_bindings" -p no:cacheprovider
+      -k "dropin or batched_bindings or concurrent_threads" -p no:cacheprovider
   timeout -k 10 200 "$A/pool_bench.bin"
   ;;
 *) echo "usage: $0 build|run" >&2; exit 2 ;;

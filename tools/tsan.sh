@@ -25,7 +25,7 @@ run)
   export TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1:suppressions=$R/tools/tsan_supp.txt"
   cd "$R"
   timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
-      -k "dropin_c_program or reentrant_threads or batched_bindings" -p no:cacheprovider
+      -k "dropin_c_program or reentrant_threads or batched_bindings or concurrent_threads" -p no:cacheprovider
   ;;
 *) echo "usage: $0 build|run" >&2; exit 2 ;;
 esac
