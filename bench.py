@@ -32,6 +32,7 @@ import argparse
 import json
 import math
 import os
+import statistics
 import sys
 import time
 
@@ -300,11 +301,12 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
         ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
         evs[2 * s + 2].record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0  # this rank's K steps; the max over ranks is taken below
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    enc_ms = sum(evs[2 * s].elapsed_ms(evs[2 * s + 1]) for s in range(args.steps)) / args.steps
-    dec_ms = sum(evs[2 * s + 1].elapsed_ms(evs[2 * s + 2]) for s in range(args.steps)) / args.steps
+    enc_t = [evs[2 * s].elapsed_ms(evs[2 * s + 1]) for s in range(args.steps)]
+    dec_t = [evs[2 * s + 1].elapsed_ms(evs[2 * s + 2]) for s in range(args.steps)]
+    enc_ms, dec_ms = sum(enc_t) / args.steps, sum(dec_t) / args.steps  # = rocprof's average
     import numpy as np
 
     ok = True  # every shard the timed steps rebuilt equals the original (on the device)
@@ -343,11 +345,12 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
                       "kAccNone,exact> (cec_encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
             "launch_ms": round(enc_ms, 4),
+            "launch_ms_median": round(statistics.median(enc_t), 4),
         },
         "decode_roofline": {
             "achieved": round(dec_gbps, 1), "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(dec_ms, 4),
-            "traffic": dec_traffic,
+            "launch_ms_median": round(statistics.median(dec_t), 4), "traffic": dec_traffic,
         },
     }
 
@@ -383,10 +386,11 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         ec.diff_update(k, m, mat, data, stage[(args.warmup + s) % 2], parity, True, plan, stream)
         evs[s + 1].record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
-    ms = sum(evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)) / args.steps
+    du_t = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
+    ms = sum(du_t) / args.steps
     chk = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
     ec.encode_region(k, m, mat, data, chk, T, stream)
     torch.cuda.synchronize()
@@ -402,7 +406,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         "workload": f"RS(3,2) {EXTRA_WORKLOADS['rs32_diff_update']}; value = SET payload (n per SET)",
         "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(gbps / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": nbytes,
-                     "launch_ms": round(ms, 4),
+                     "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(du_t), 4),
                      "kernel": "combine_kernel<2,3,*,kAccAllButLast,exact> (cec_diff_update, install)",
                      "traffic": load_traffic("rs32_diff_update", ("diff_update",))[0]},
         "verified": bool(ok and bad == 0.0),
@@ -508,9 +512,9 @@ def measure_e2e(torch, dist, ec, world, rank, args):
     for _ in range(steps):
         e.step()
     torch.cuda.synchronize()
+    el = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
     h2d, d2h = pcie_raw(torch)
     floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
     el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
@@ -946,9 +950,9 @@ def run_harness_check(args):
         dist.barrier()
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))  # ranks finish at different times: the max must win
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     mine = [float(elapsed), float(0.01 * (rank + 1)), float(rank)]
     got = max_over_ranks(mine, dist if world > 1 else None)
     spans = [None] * world
