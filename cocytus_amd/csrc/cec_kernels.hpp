@@ -263,8 +263,8 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
         const int n_in = kExact ? NT : P->n_in;
         const int n_out = kExact ? LT : P->n_out;
         if (!kExact && n_out == 0) continue;
-        // A workgroup that walks several tiles (more than 2^31 work items) must not
-        // re-stage LDS rows while lanes still read the previous tile's.
+        // A workgroup that walks several tiles (a launch past one dispatch's 2^32 - 1
+        // work items) must not re-stage LDS rows while lanes still read the previous tile's.
         if constexpr (Eng::kStaged)
             if (g != blockIdx.x) __syncthreads();
         auto is_acc = [&](int l) -> bool {

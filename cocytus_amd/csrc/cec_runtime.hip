@@ -410,7 +410,10 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     a.split_shift = split_shift_for(st, plan);
     const size_t lds_bytes = std::max(lds ? static_cast<size_t>(max_rows) * 256 : 0,
                                       occupancy_lds(dev, a.split_shift));
-    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, 0x7FFFFFFFull));
+    // A dispatch holds at most 2^32 - 1 work items per dimension: past that (more than
+    // 64 GiB of tiles per stream) workgroups walk the rest grid-stride.
+    const uint64_t max_wgs = 0xFFFFFFFFull / (kBlock >> a.split_shift);
+    const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, max_wgs));
     int en, el, eacc;
     const bool exact = exact_shape(pats, used, &en, &el, &eacc) &&
                        (lds ? launch_exact<LdsEngine>(en, el, eacc, a, grid, lds_bytes, stream)

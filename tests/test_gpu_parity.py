@@ -86,6 +86,40 @@ def test_region_multiply_in_place(gpu, oracle):
     assert np.array_equal(to_host(d), exp)
 
 
+def test_region_multiply_past_one_dispatch(gpu, oracle, engine):
+    """Maximum sizes: 64 GiB + 3 tiles + 77 B per stream is more than one dispatch's
+    2^32 - 1 work items, so the grid is capped and workgroups walk the rest grid-stride
+    (run_combine).  Windows at the head, the tail and across the first tiles past the
+    cap (offset 2^36 = tile 2^24) are checked against the oracle; then x ^= c * src again
+    must leave every byte 0 (size-independent: a tile skipped in either pass leaves the
+    0xFF fill or c * src)."""
+    torch, ec = gpu
+    n = (1 << 36) + 3 * 4096 + 77
+    torch.cuda.empty_cache()
+    ec.cache_trim()
+    if torch.cuda.mem_get_info()[0] < 2 * n + (4 << 30):
+        pytest.skip("needs 2 x 64 GiB of free HBM")
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70007)
+    src = torch.empty(n, dtype=torch.uint8, device="cuda")
+    src.random_(0, 256, generator=g)
+    dst = torch.full((n,), 0xFF, dtype=torch.uint8, device="cuda")
+    c, W = 0x53, 1 << 20
+    try:
+        ec.region_multiply(src, c, n, dst, 0)
+        torch.cuda.synchronize()
+        rng = np.random.default_rng(7)
+        for off in [0, n - W, (1 << 36) - W + 8192, *rng.integers(0, n - W, 4).tolist()]:
+            exp = np.zeros(W, dtype=np.uint8)
+            oracle.region_multiply(to_host(src[off:off + W]), c, exp, 0)
+            assert np.array_equal(to_host(dst[off:off + W]), exp), off
+        ec.region_multiply(src, c, n, dst, 1)
+        torch.cuda.synchronize()
+        assert not bool(dst.any())
+    finally:
+        del src, dst
+        torch.cuda.empty_cache()
+
+
 # ------------------------------------------------------------------ encode (a5)
 @pytest.mark.parametrize("k,m", CODES)
 def test_encode_plan(gpu, oracle, engine, k, m):
