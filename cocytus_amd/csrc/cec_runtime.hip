@@ -573,6 +573,73 @@ CEC_API int cec_set_waves_per_cu(int waves_per_cu) {
 CEC_API int cec_get_waves_per_cu(void) { return waves_per_cu_cap(); }
 
 // ============================================================== ops
+// Region multiply (one input, one output, an implicit region) without the generic path:
+// the tables of a thread's last (device, multby, add, engine) stay pinned in the cache
+// and memoised, so a call skips building, copying and hashing its 1.7 KiB pattern and
+// the lookup (tools/dropin_breakdown.hip: 3.4 us of host time per call against 0.9 us
+// for an empty launch).  The memo is used on another stream only once the tables'
+// upload is known complete, and never while capturing (the cache then marks them).
+namespace {
+struct RegionMemo {
+    int dev = -1, key = -1;
+    hipStream_t stream = nullptr;  // the stream the tables were made ready for
+    PatEntry *e = nullptr;         // pinned while memoised
+    LaunchShape shape;
+    ~RegionMemo() {
+        if (e) pattern_done(e);
+    }
+};
+thread_local RegionMemo t_region;
+}  // namespace
+
+// `plain`: s is known not to be capturing (the drop-in's private stream).
+static int region_launch(int dev, const void *src, int multby, size_t n, void *dst, int add, hipStream_t s,
+                         bool plain) {
+    const uint64_t n_tiles = (n + kTile - 1) / kTile;
+    if (n_tiles > 0xFFFFFFFFull) return fail(CEC_EINVAL, "region too large");
+    const int engine = g_engine.load();
+    const int key = (engine << 9) | (add ? 256 : 0) | multby;
+    const bool capturing = !plain && stream_capturing(s);
+    RegionMemo &m = t_region;
+    Streams st;
+    st.base[0] = static_cast<uint8_t *>(const_cast<void *>(src));
+    st.base[1] = static_cast<uint8_t *>(dst);
+    if (!(m.e && m.dev == dev && m.key == key && !capturing &&
+          (s == m.stream || m.e->up_done.load(std::memory_order_acquire)))) {
+        Combo cb;
+        cb.n_in = 1;
+        cb.in_stream[0] = 0;
+        Combo::Out o{};
+        o.stream = 1;
+        o.mode = add ? kModeXor : kModeWrite;
+        o.coef[0] = multby;
+        cb.outs.push_back(o);
+        std::vector<Pattern> pats;
+        std::vector<uint8_t> rows;
+        build_patterns({cb}, 0, engine, pats, rows);
+        std::string k(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
+        k.append(reinterpret_cast<const char *>(rows.data()), rows.size());
+        PatEntry *e = nullptr;
+        if (int r = pattern_get(dev, std::move(k), s, &e)) return r;
+        if (capturing) {  // tables now marked captured: pinned for this launch only
+            launch_combine(dev, st, e->d, 1, launch_shape(pats, nullptr), engine == CEC_ENGINE_LDS, nullptr, n,
+                           n_tiles, s);
+            pattern_done(e);
+            HIP_TRY(hipGetLastError());
+            return CEC_OK;
+        }
+        if (m.e) pattern_done(m.e);  // this launch's pin becomes the memo's
+        m.dev = dev;
+        m.key = key;
+        m.stream = s;
+        m.e = e;
+        m.shape = launch_shape(pats, nullptr);
+    }
+    launch_combine(dev, st, m.e->d, 1, m.shape, engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s);
+    HIP_TRY(hipGetLastError());
+    return CEC_OK;
+}
+
 CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void *dst, int add,
                                 void *stream) {
     if (!src || multby < 0 || multby > 255) return fail(CEC_EINVAL, "cec_region_multiply: bad args");
@@ -584,18 +651,7 @@ CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void
         add = 0;
     }
     if (add && multby == 0) return CEC_OK;
-    Streams st;
-    st.base[0] = static_cast<uint8_t *>(const_cast<void *>(src));
-    st.base[1] = static_cast<uint8_t *>(dst);
-    Combo c;
-    c.n_in = 1;
-    c.in_stream[0] = 0;
-    Combo::Out o{};
-    o.stream = 1;
-    o.mode = add ? kModeXor : kModeWrite;
-    o.coef[0] = multby;
-    c.outs.push_back(o);
-    return run_combos(dev, st, {c}, nullptr, nbytes, static_cast<hipStream_t>(stream));
+    return region_launch(dev, src, multby, nbytes, dst, add, static_cast<hipStream_t>(stream), false);
 }
 
 static int encode_common(int k, int m, const int *matrix, const uint8_t *const *data,
@@ -1100,11 +1156,6 @@ struct DropInCtx {
     uint8_t *zc = nullptr;  // mapped pinned buffer (2 x zc_cap) for zero-copy calls
     void *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
-    // The tables of the last (multby, add, engine), pinned in the cache (so never evicted
-    // under this thread) with the kernel shape they take.
-    PatEntry *pat = nullptr;
-    int pat_memo = -1;
-    LaunchShape pat_shape;
     ~DropInCtx() {
         if (stream) {
             (void)hipStreamSynchronize(stream);
@@ -1121,9 +1172,6 @@ struct DropInCtx {
         dsrc = ddst = zc = nullptr;
         zc_dev = nullptr;
         cap = zc_cap = 0;
-        if (pat) pattern_done(pat);
-        pat = nullptr;
-        pat_memo = -1;
     }
 };
 thread_local DropInCtx t_ctx;
@@ -1138,44 +1186,6 @@ size_t zero_copy_max() {
         return e ? static_cast<size_t>(strtoull(e, nullptr, 0)) : size_t(256) << 10;
     }();
     return v;
-}
-
-// dst (^)= multby * src over n bytes of device-usable memory, on the thread's drop-in
-// stream.  It is cec_region_multiply without the generic path: the pattern of the last
-// (multby, add, engine) is memoised per thread, so a call skips building, hashing and
-// looking up its tables (tools/dropin_breakdown.hip: the library's host time per call
-// was 3.4 us against 0.9 us for an empty launch).
-int dropin_launch(DropInCtx &c, int dev, void *src, int multby, size_t n, void *dst, int add) {
-    const int engine = g_engine.load();
-    const int memo = (engine << 9) | (add ? 256 : 0) | multby;
-    if (!c.pat || c.pat_memo != memo) {
-        Combo cb;
-        cb.n_in = 1;
-        cb.in_stream[0] = 0;
-        Combo::Out o{};
-        o.stream = 1;
-        o.mode = add ? kModeXor : kModeWrite;
-        o.coef[0] = multby;
-        cb.outs.push_back(o);
-        std::vector<Pattern> pats;
-        std::vector<uint8_t> rows;
-        build_patterns({cb}, 0, engine, pats, rows);
-        std::string key(reinterpret_cast<const char *>(pats.data()), pats.size() * sizeof(Pattern));
-        key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
-        PatEntry *e = nullptr;
-        if (int r = pattern_get(dev, std::move(key), c.stream, &e)) return r;
-        if (c.pat) pattern_done(c.pat);  // (stays pinned: this thread launches with it)
-        c.pat = e;
-        c.pat_memo = memo;
-        c.pat_shape = launch_shape(pats, nullptr);
-    }
-    Streams st;
-    st.base[0] = static_cast<uint8_t *>(src);
-    st.base[1] = static_cast<uint8_t *>(dst);
-    launch_combine(dev, st, c.pat->d, 1, c.pat_shape, engine == CEC_ENGINE_LDS, nullptr, n, (n + kTile - 1) / kTile,
-                   c.stream);
-    HIP_TRY(hipGetLastError());
-    return CEC_OK;
 }
 
 // Device-usable address for p, or NULL if p is pageable host memory.
@@ -1232,7 +1242,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     const int mode_add = r2 ? add : 0;
     void *vs = device_view(region), *vd = device_view(dst);
     if (vs && vd) {  // device-resident (or pinned/mapped): run in place
-        DROPIN_CHECK(dropin_launch(c, dev, vs, multby, n, vd, mode_add));
+        DROPIN_CHECK(region_launch(dev, vs, multby, n, vd, mode_add, c.stream, true));
         DROPIN_CHECK(stream_wait(c.stream));
         return;
     }
@@ -1248,7 +1258,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         memcpy(zs, region, n);
         if (mode_add) memcpy(zd, dst, n);
         uint8_t *ds = static_cast<uint8_t *>(c.zc_dev), *dd = ds + c.zc_cap;
-        DROPIN_CHECK(dropin_launch(c, dev, ds, multby, n, dd, mode_add));
+        DROPIN_CHECK(region_launch(dev, ds, multby, n, dd, mode_add, c.stream, true));
         DROPIN_CHECK(stream_wait(c.stream));  // (spinning on hipStreamQuery instead: no gain)
         memcpy(dst, zd, n);
         return;
@@ -1268,7 +1278,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         DROPIN_HIP(hipMemcpyAsync(c.dsrc, region + o, len, hipMemcpyHostToDevice, c.stream));
         if (mode_add)
             DROPIN_HIP(hipMemcpyAsync(c.ddst, dst + o, len, hipMemcpyHostToDevice, c.stream));
-        DROPIN_CHECK(dropin_launch(c, dev, c.dsrc, multby, len, c.ddst, mode_add));
+        DROPIN_CHECK(region_launch(dev, c.dsrc, multby, len, c.ddst, mode_add, c.stream, true));
         DROPIN_HIP(hipMemcpyAsync(dst + o, c.ddst, len, hipMemcpyDeviceToHost, c.stream));
         DROPIN_HIP(hipStreamSynchronize(c.stream));
     }
