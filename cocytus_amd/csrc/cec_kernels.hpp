@@ -71,15 +71,25 @@ struct Tile {
     uint32_t pattern;
 };
 
-struct CombineArgs {
-    uint8_t *base[kMaxStreams];
+// Kernel arguments with S stream slots.  Patterns name streams by slot.  The host
+// writes a launch's whole kernarg segment for every dispatch, and 424 B of arguments
+// cost 1.3 us more host time per launch than none (tools/dropin_breakdown.hip).  So a
+// launch whose patterns use only slots 0 and 1 (region multiply, the drop-in) takes
+// S = 2, and the kernel reads its grid size from here rather than from gridDim /
+// blockDim: those come from the hidden arguments, which add 256 B to every segment.
+template <int S>
+struct CombineArgsN {
+    uint8_t *base[S];
     const Tile *tiles;       // NULL: implicit region [0, implicit_len), pattern 0
     const Pattern *patterns;
     const uint8_t *rows;     // LDS engine: 256-B product rows (c*x for x = 0..255)
     uint64_t implicit_len;
     uint32_t n_tiles;
     uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
+    uint32_t grid;         // workgroups in the launch (the grid-stride step)
 };
+using CombineArgs = CombineArgsN<kMaxStreams>;
+constexpr int kNarrowStreams = 2;
 
 #define CEC_CONST __attribute__((address_space(4)))
 #define CEC_GLOBAL __attribute__((address_space(1)))
@@ -161,7 +171,8 @@ struct TileRef {
     uint32_t pattern;
 };
 
-__device__ inline TileRef load_tile(const CombineArgs &a, uint32_t t) {
+template <class A>
+__device__ inline TileRef load_tile(const A &a, uint32_t t) {
     TileRef r;
     if (a.tiles == nullptr) {
         const uint64_t o = static_cast<uint64_t>(t) * kTile;
@@ -247,14 +258,14 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 
 // A workgroup covers 1 / 2^split_shift of a tile (blockDim = kBlock >> split_shift):
 // work item g is tile g >> split_shift, part g & (2^split_shift - 1).
-template <int NT, int LT, class Eng, int kAcc, bool kExact>
-__global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
+template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams>
+__global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
     extern __shared__ uint4 cec_lds_rows[];  // LDS engine: the pattern's product rows
     const uint8_t *lds = reinterpret_cast<const uint8_t *>(cec_lds_rows);
     const uint32_t sh = a.split_shift;
     const uint64_t n_work = static_cast<uint64_t>(a.n_tiles) << sh;
 
-    for (uint64_t g = blockIdx.x; g < n_work; g += gridDim.x) {
+    for (uint64_t g = blockIdx.x; g < n_work; g += a.grid) {
         const uint32_t t = static_cast<uint32_t>(g >> sh);
         const uint32_t part = static_cast<uint32_t>(g) & ((1u << sh) - 1u);
         const uint32_t lane = (part << (kBlockLog2 - sh)) + threadIdx.x;
@@ -334,7 +345,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgs a) {
             const uint32_t nb = static_cast<uint32_t>(P->lds_rows) * 256u;
             if (nb) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
-                for (uint32_t b = threadIdx.x; b < nb / 16; b += blockDim.x) cec_lds_rows[b] = src[b];
+                for (uint32_t b = threadIdx.x; b < nb / 16; b += kBlock >> sh) cec_lds_rows[b] = src[b];
                 __syncthreads();
             }
             if (!active) continue;

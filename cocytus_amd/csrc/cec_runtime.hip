@@ -143,10 +143,29 @@ static void assign_rows(Pattern &p, std::vector<uint8_t> &rows) {
 
 // ============================================================== launch
 // `lds`: dynamic LDS bytes of the launch (LDS engine: the largest pattern's rows).
-template <int NT, int LT, class Eng, int kAcc, bool kExact>
-static void launch_k(const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact>), dim3(grid),
+template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams>
+static void launch_k(const CombineArgsN<S> &a, int grid, size_t lds, hipStream_t s) {
+    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact, S>), dim3(grid),
                        dim3(kBlock >> a.split_shift), lds, s, a);
+}
+
+// The 1 x 1 shapes (region multiply-XOR / write, parity apply) with the two-slot
+// arguments, for launches whose patterns use slots 0 and 1 only.
+template <class Eng>
+static bool launch_narrow(int acc, const CombineArgs &w, int grid, size_t lds, hipStream_t s) {
+    CombineArgsN<kNarrowStreams> a;
+    for (int i = 0; i < kNarrowStreams; ++i) a.base[i] = w.base[i];
+    a.tiles = w.tiles;
+    a.patterns = w.patterns;
+    a.rows = w.rows;
+    a.implicit_len = w.implicit_len;
+    a.n_tiles = w.n_tiles;
+    a.split_shift = w.split_shift;
+    a.grid = w.grid;
+    if (acc == kAccAll) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams>(a, grid, lds, s);
+    else if (acc == kAccNone) launch_k<1, 1, Eng, kAccNone, true, kNarrowStreams>(a, grid, lds, s);
+    else return false;
+    return true;
 }
 
 // Exact-shape kernels for the hot ops: encode / decode / residual / solve (no RMW,
@@ -373,6 +392,7 @@ struct LaunchShape {
     int nt = 1, lt = 0, max_rows = 0;
     bool exact = false;
     int en = 0, el = 0, eacc = 0;
+    int streams = 0;  // 1 + the highest stream slot a used pattern names
 };
 
 static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vector<char> *used) {
@@ -382,6 +402,8 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
         sh.nt = std::max(sh.nt, pats[i].n_in);
         sh.lt = std::max(sh.lt, pats[i].n_out);
         sh.max_rows = std::max(sh.max_rows, pats[i].lds_rows);
+        for (int j = 0; j < pats[i].n_in; ++j) sh.streams = std::max(sh.streams, pats[i].in_stream[j] + 1);
+        for (int j = 0; j < pats[i].n_out; ++j) sh.streams = std::max(sh.streams, pats[i].out_stream[j] + 1);
     }
     sh.exact = exact_shape(pats, used, &sh.en, &sh.el, &sh.eacc);
     return sh;
@@ -412,6 +434,11 @@ static void launch_combine(int dev, const Streams &st, const uint8_t *tables, si
     // 64 GiB of tiles per stream) workgroups walk the rest grid-stride.
     const uint64_t max_wgs = 0xFFFFFFFFull / (kBlock >> a.split_shift);
     const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, max_wgs));
+    a.grid = static_cast<uint32_t>(grid);
+    if (sh.exact && sh.en == 1 && sh.el == 1 && sh.streams <= kNarrowStreams &&
+        (lds ? launch_narrow<LdsEngine>(sh.eacc, a, grid, lds_bytes, stream)
+             : launch_narrow<PermEngine>(sh.eacc, a, grid, lds_bytes, stream)))
+        return;
     const bool exact = sh.exact &&
                        (lds ? launch_exact<LdsEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream)
                             : launch_exact<PermEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream));

@@ -7,6 +7,8 @@
 //   empty     an empty kernel launch: host time of the call alone
 //   bigarg    the same with a 424-B by-value argument (CombineArgs' size)
 //   capturing hipStreamIsCapturing on a plain stream
+//   devcount  hipGetDeviceCount;  lasterr  hipGetLastError
+//   arg64     a launch with a 64-B by-value argument (the two-slot arguments' size)
 //   dev_call  galois_w08_region_multiply on device pointers, 4 KiB (launch + wait)
 //   pageable  galois_w08_region_multiply on malloc'd buffers, 64 B and 4 KiB
 #include <hip/hip_runtime.h>
@@ -24,6 +26,10 @@ struct BigArgs {  // the size of the library's CombineArgs (48 stream bases + fi
     void *p[53];
 };
 __global__ void bigarg_kernel(BigArgs a) { (void)a; }
+struct SmallArgs {
+    void *p[8];
+};
+__global__ void arg64_kernel(SmallArgs a) { (void)a; }
 
 using clk = std::chrono::steady_clock;
 static double us_since(clk::time_point t0, int n) {
@@ -64,13 +70,22 @@ int main() {
     for (int i = 0; i < N; ++i) (void)hipGetDevice(&dev);
     const double getdev = us_since(t0, N);
 
+    int cnt = 0;
+    t0 = clk::now();
+    for (int i = 0; i < N; ++i) (void)hipGetDeviceCount(&cnt);
+    const double devcount = us_since(t0, N);
+    t0 = clk::now();
+    for (int i = 0; i < N; ++i) (void)hipGetLastError();
+    const double lasterr = us_since(t0, N);
+
     hipStreamCaptureStatus cs;
     t0 = clk::now();
     for (int i = 0; i < N; ++i) (void)hipStreamIsCapturing(s, &cs);
     const double capt = us_since(t0, N);
 
-    double enq = 0, emp = 0, big = 0;
+    double enq = 0, emp = 0, big = 0, a64 = 0;
     BigArgs ba{};
+    SmallArgs sa{};
     for (int r = 0; r < N / 64; ++r) {
         auto t1 = clk::now();
         for (int i = 0; i < 64; ++i) cec_region_multiply(d1, 3, 4096, d2, 1, s);
@@ -84,10 +99,15 @@ int main() {
         for (int i = 0; i < 64; ++i) hipLaunchKernelGGL(bigarg_kernel, dim3(1), dim3(64), 0, s, ba);
         big += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
         CK(hipStreamSynchronize(s));
+        t1 = clk::now();
+        for (int i = 0; i < 64; ++i) hipLaunchKernelGGL(arg64_kernel, dim3(4), dim3(64), 0, s, sa);
+        a64 += std::chrono::duration<double, std::micro>(clk::now() - t1).count();
+        CK(hipStreamSynchronize(s));
     }
     enq /= (N / 64) * 64;
     emp /= (N / 64) * 64;
     big /= (N / 64) * 64;
+    a64 /= (N / 64) * 64;
 
     t0 = clk::now();
     for (int i = 0; i < N / 4; ++i)
@@ -101,9 +121,10 @@ int main() {
         for (int i = 0; i < N / 4; ++i) galois_w08_region_multiply(h, 3, sizes[z], h2, 1);
         pg[z] = us_since(t0, N / 4);
     }
-    printf("{\"attr_us\": %.3f, \"getdev_us\": %.3f, \"capturing_us\": %.3f, \"enqueue_us\": %.3f, "
-           "\"empty_launch_us\": %.3f, \"bigarg_launch_us\": %.3f, \"dev_call_4k_us\": %.2f, "
+    printf("{\"attr_us\": %.3f, \"getdev_us\": %.3f, \"devcount_us\": %.3f, \"lasterr_us\": %.3f, "
+           "\"capturing_us\": %.3f, \"enqueue_us\": %.3f, \"empty_launch_us\": %.3f, "
+           "\"arg64_launch_us\": %.3f, \"bigarg_launch_us\": %.3f, \"dev_call_4k_us\": %.2f, "
            "\"pageable_64_us\": %.2f, \"pageable_4k_us\": %.2f}\n",
-           attr, getdev, capt, enq, emp, big, devcall, pg[0], pg[1]);
+           attr, getdev, devcount, lasterr, capt, enq, emp, a64, big, devcall, pg[0], pg[1]);
     return 0;
 }
