@@ -604,13 +604,13 @@ CEC_API int cec_get_waves_per_cu(void) { return waves_per_cu_cap(); }
 // the tables of a thread's last (device, multby, add, engine) stay pinned in the cache
 // and memoised, so a call skips building, copying and hashing its 1.7 KiB pattern and
 // the lookup (tools/dropin_breakdown.hip: 3.4 us of host time per call against 0.9 us
-// for an empty launch).  The memo is used on another stream only once the tables'
-// upload is known complete, and never while capturing (the cache then marks them).
+// for an empty launch).  The memo is used only once the tables' upload is known
+// complete (until then the cache orders each launch after it), and never while
+// capturing (the cache then marks the tables).
 namespace {
 struct RegionMemo {
     int dev = -1, key = -1;
-    hipStream_t stream = nullptr;  // the stream the tables were made ready for
-    PatEntry *e = nullptr;         // pinned while memoised
+    PatEntry *e = nullptr;  // pinned while memoised
     LaunchShape shape;
     ~RegionMemo() {
         if (e) pattern_done(e);
@@ -631,8 +631,7 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
     Streams st;
     st.base[0] = static_cast<uint8_t *>(const_cast<void *>(src));
     st.base[1] = static_cast<uint8_t *>(dst);
-    if (!(m.e && m.dev == dev && m.key == key && !capturing &&
-          (s == m.stream || m.e->up_done.load(std::memory_order_acquire)))) {
+    if (!(m.e && m.dev == dev && m.key == key && !capturing && m.e->up_done.load(std::memory_order_acquire))) {
         Combo cb;
         cb.n_in = 1;
         cb.in_stream[0] = 0;
@@ -658,7 +657,6 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
         if (m.e) pattern_done(m.e);  // this launch's pin becomes the memo's
         m.dev = dev;
         m.key = key;
-        m.stream = s;
         m.e = e;
         m.shape = launch_shape(pats, nullptr);
     }
