@@ -645,6 +645,71 @@ def test_dropin_reentrant_threads(gpu, tmp_path):
     assert "0 mismatches" in out
 
 
+@pytest.fixture
+def resident(gpu):
+    """The drop-in's resident worker on for one test (cocytus_ec.h), off afterwards."""
+    _, ec = gpu
+    ec.set_dropin_resident(True)
+    yield ec
+    ec.set_dropin_resident(False)
+
+
+def test_dropin_resident_worker(resident, oracle):
+    """Small pageable calls through the resident worker: every size up to its 16 KiB
+    limit's edges, both modes, every kind of coefficient, vs the oracle; then beyond the
+    limit, device buffers and the staged path interleaved (each stops the worker first),
+    and gaps longer than its idle timeout (it leaves and is relaunched)."""
+    import time
+
+    ec = resident
+    assert ec.get_dropin_resident()
+    rng = np.random.default_rng(0x5E5)
+    sizes = [1, 2, 15, 16, 17, 4095, 4096, 4098, 8191, 12289, 16383, 16384, 16385, 70000]
+    for it in range(6):
+        for n in sizes:
+            c = int(rng.choice([0, 1, 2, 0x80, 244, 245, 255, int(rng.integers(0, 256))]))
+            add = int(it % 2 == 0 or n % 3 == 0)
+            a = rng.integers(0, 256, n, dtype=np.uint8)
+            b = rng.integers(0, 256, n, dtype=np.uint8)
+            exp = b.copy() if add else np.zeros(n, np.uint8)
+            oracle.region_multiply(a, c, exp, 1)
+            ec.galois_w08_region_multiply(a, c, n, b, add)
+            assert np.array_equal(b, exp), (it, n, c, add)
+        if it == 2:
+            time.sleep(0.01)  # past the idle timeout: the next call relaunches the worker
+
+
+def test_dropin_resident_stress(resident, oracle):
+    """20,000 back-to-back 4 KiB-ish calls on the same staging (every call's bytes new):
+    a stale line anywhere in the mailbox or staging path shows up as a mismatch.  The
+    worker's 5 ms lifetime runs out several times on the way (relaunch under load)."""
+    ec = resident
+    rng = np.random.default_rng(0x57E55)
+    n_calls = 20000
+    a_all = rng.integers(0, 256, (64, 4098), dtype=np.uint8)
+    b_all = rng.integers(0, 256, (64, 4098), dtype=np.uint8)
+    cs = rng.integers(0, 256, n_calls)
+    bad = 0
+    for i in range(n_calls):
+        a, b0, c = a_all[i % 64], b_all[(i * 7) % 64], int(cs[i])
+        n = 4096 + (i % 3)
+        b = b0[:n].copy()
+        exp = b.copy()
+        oracle.region_multiply(a[:n], c, exp, 1)
+        ec.galois_w08_region_multiply(a, c, n, b, 1)
+        bad += int(not np.array_equal(b, exp))
+    assert bad == 0
+
+
+def test_dropin_resident_threads(gpu, tmp_path):
+    """The 8-thread re-entrancy program with the resident worker on: one thread owns the
+    worker, the others launch; sizes cross the worker's limit and the staged path."""
+    from tests.dropin import run_dropin_threads
+
+    out = run_dropin_threads(tmp_path, threads=8, iters=150, env={"CEC_DROPIN_RESIDENT": "1"})
+    assert "0 mismatches" in out
+
+
 def test_arena_allocator(gpu, oracle):
     """cec_arenas_alloc: count arenas at an odd-4 KiB stride, usable by every op."""
     import ctypes
