@@ -981,8 +981,10 @@ struct SignalCtx {  // per thread and device: a mapped pinned completion word
     int device = -1;
     uint32_t *flag = nullptr, *flag_dev = nullptr;
     uint32_t seq = 0;
+    hipEvent_t fence = nullptr;  // recorded before the signal: a system-scope release
     ~SignalCtx() {  // (idle: every wait completed before its call returned)
         map_cache().release(device, flag, 64);
+        if (fence) (void)hipEventDestroy(fence);
     }
 };
 thread_local SignalCtx t_signal;
@@ -1007,9 +1009,18 @@ static int stream_wait(hipStream_t s) {
         HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&c.flag_dev), c.flag, 0));
         __atomic_store_n(c.flag, 0u, __ATOMIC_RELEASE);
         c.seq = 0;
+        if (c.fence) (void)hipEventDestroy(c.fence);
+        c.fence = nullptr;
+        HIP_TRY(hipEventCreateWithFlags(&c.fence, hipEventDisableTiming));
         c.device = dev;
     }
     const uint32_t v = ++c.seq;
+    // The op's stores into host memory may still sit in the L2 of the XCDs its
+    // workgroups ran on, and the signal kernel's own fence writes back only its XCD's
+    // (a 4098-byte drop-in call read back its second tile stale on some boxes).  An
+    // event recorded with the system fence makes the command processor write every L2
+    // back before the signal kernel starts.
+    HIP_TRY(hipEventRecord(c.fence, s));
     hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
     HIP_TRY(hipGetLastError());
     const auto t0 = std::chrono::steady_clock::now();
@@ -1171,10 +1182,7 @@ CEC_API int *jerasure_matrix_multiply(int *m1, int *m2, int r1, int c1, int r2, 
     return p;
 }
 
-#include "cec_resident.inc"
-
-// Per-thread context of the synchronous drop-in: a stream, device staging, and (the
-// owning thread only) the resident worker's mailbox and stream.
+// Per-thread context of the synchronous drop-in: a stream and device staging.
 namespace {
 struct DropInCtx {
     int device = -1;
@@ -1184,12 +1192,6 @@ struct DropInCtx {
     uint8_t *zc = nullptr;  // mapped pinned buffer (2 x zc_cap) for zero-copy calls
     void *zc_dev = nullptr;  // its device address
     size_t zc_cap = 0;
-    // resident worker (cec_resident.inc)
-    bool res_owner = false, res_alive = false;
-    hipStream_t res_stream = nullptr;
-    ResMailbox *mb = nullptr, *mb_dev = nullptr;
-    uint32_t res_gen = 0, res_seq = 0;
-    uint64_t idle_ticks = 0, life_ticks = 0;
     ~DropInCtx() {
         if (stream) {
             (void)hipStreamSynchronize(stream);
@@ -1200,128 +1202,12 @@ struct DropInCtx {
     // Buffers back to the process caches (idle: every call completed before returning);
     // freeing them would wait for the whole device.
     void release() {
-        resident_release();
         dev_cache().release(device, dsrc, cap);
         dev_cache().release(device, ddst, cap);
         map_cache().release(device, zc, 2 * zc_cap);
         dsrc = ddst = zc = nullptr;
         zc_dev = nullptr;
         cap = zc_cap = 0;
-    }
-
-    // This thread may use the resident worker of device dev (mode on, and it holds, or
-    // now takes, the device's one worker slot); sets the mailbox up on first use.  The
-    // zero-copy staging (>= kResMax per side) must exist.
-    bool resident_ready(int dev) {
-        if (!g_resident_mode.load(std::memory_order_relaxed)) {
-            resident_quiesce();
-            return false;
-        }
-        if (res_owner) return true;
-        bool expect = false;
-        if (!g_resident_owned[dev].compare_exchange_strong(expect, true)) return false;
-        mb = static_cast<ResMailbox *>(map_cache().acquire(dev, sizeof(ResMailbox)));
-        int khz = 0;
-        if (!mb || hipHostGetDevicePointer(reinterpret_cast<void **>(&mb_dev), mb, 0) != hipSuccess ||
-            hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0 ||
-            hipStreamCreateWithFlags(&res_stream, hipStreamNonBlocking) != hipSuccess) {
-            (void)hipGetLastError();
-            if (mb) map_cache().release(dev, mb, sizeof(ResMailbox));
-            mb = mb_dev = nullptr;
-            res_stream = nullptr;
-            g_resident_owned[dev].store(false);
-            return false;
-        }
-        memset(mb, 0, sizeof(ResMailbox));
-        __atomic_thread_fence(__ATOMIC_SEQ_CST);
-        const uint64_t per_us = static_cast<uint64_t>(khz) / 1000u;
-        tick_us = 1000.0 / khz;
-        idle_ticks = std::max<uint64_t>(resident_env_us("CEC_RESIDENT_IDLE_US", 1000), 20) * per_us;
-        life_ticks = std::max<uint64_t>(resident_env_us("CEC_RESIDENT_LIFE_US", 5000), 100) * per_us;
-        res_gen = res_seq = 0;
-        res_alive = false;
-        res_owner = true;
-        return true;
-    }
-    void resident_launch(uint32_t last) {
-        ++res_gen;
-        uint8_t *ds = static_cast<uint8_t *>(zc_dev);
-        hipLaunchKernelGGL(cec_resident_kernel, dim3(1), dim3(kResThreads), 0, res_stream, mb_dev, ds, ds + zc_cap,
-                           res_gen, last, idle_ticks, life_ticks);
-        const hipError_t e = hipGetLastError();
-        if (e != hipSuccess) {
-            char b[256];
-            snprintf(b, sizeof b, "galois_w08_region_multiply: resident worker launch: %s", hipGetErrorString(e));
-            die(b);
-        }
-        res_alive = true;
-    }
-    // zd = (add ? zd : 0) ^ c * zs over the first n bytes of the zero-copy staging.
-    void resident_call(int multby, size_t n, int add) {
-        ResMailbox *m = mb;
-        const PermTab t = make_perm_tab(multby);
-        m->n = static_cast<uint32_t>(n);
-        m->add = static_cast<uint32_t>(add);
-        for (int i = 0; i < 5; ++i) m->tab[i] = t.w[i];
-        const uint32_t s = ++res_seq;
-        __atomic_store_n(&m->seq, s, __ATOMIC_RELEASE);  // (the staging bytes were written before)
-        if (!res_alive || __atomic_load_n(&m->exited_gen, __ATOMIC_ACQUIRE) == res_gen) resident_launch(s - 1);
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t i = 1;; ++i) {
-            if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == s) {
-                if (trace) trace_add(m, std::chrono::steady_clock::now() - t0);
-                return;
-            }
-            __builtin_ia32_pause();
-            if ((i & 255) != 0) continue;
-            if (__atomic_load_n(&m->exited_gen, __ATOMIC_ACQUIRE) == res_gen) {
-                // the worker left (idle / life); it acknowledges before it leaves
-                if (__atomic_load_n(&m->done, __ATOMIC_ACQUIRE) == s) return;
-                resident_launch(s - 1);
-            }
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-                const hipError_t e = hipStreamQuery(res_stream);
-                char b[256];
-                snprintf(b, sizeof b, "galois_w08_region_multiply: resident worker did not reply in 10 s (%s)",
-                         hipGetErrorString(e));
-                die(b);
-            }
-        }
-    }
-    // Stop the worker and wait for it to leave (before the thread's other paths use the
-    // GPU: its stream may share a hardware queue with this thread's other stream).
-    void resident_quiesce() {
-        if (!res_alive) return;
-        __atomic_store_n(&mb->stop, 1u, __ATOMIC_RELEASE);
-        (void)hipStreamSynchronize(res_stream);
-        (void)hipGetLastError();
-        __atomic_store_n(&mb->stop, 0u, __ATOMIC_RELEASE);
-        res_alive = false;
-    }
-    // CEC_RESIDENT_TRACE: per-request phase times, averaged and printed at release
-    bool trace = getenv("CEC_RESIDENT_TRACE") != nullptr;
-    double tr_n = 0, tr_host = 0, tr_poll = 0, tr_load = 0, tr_store = 0, tick_us = 0.01;
-    void trace_add(const ResMailbox *m, std::chrono::steady_clock::duration d) {
-        tr_n += 1;
-        tr_host += std::chrono::duration<double, std::micro>(d).count();
-        tr_poll += m->t_poll * tick_us;
-        tr_load += m->t_load * tick_us;
-        tr_store += m->t_store * tick_us;
-    }
-    void resident_release() {
-        if (trace && tr_n > 0)
-            fprintf(stderr,
-                    "{\"resident_trace\": {\"requests\": %.0f, \"host_post_to_done_us\": %.2f, \"poll_read_us\": %.2f, "
-                    "\"load_us\": %.2f, \"store_drain_us\": %.2f, \"launches\": %u}}\n",
-                    tr_n, tr_host / tr_n, tr_poll / tr_n, tr_load / tr_n, tr_store / tr_n, res_gen);
-        if (!res_owner) return;
-        resident_quiesce();
-        (void)hipStreamDestroy(res_stream);
-        map_cache().release(device, mb, sizeof(ResMailbox));
-        mb = mb_dev = nullptr;
-        res_stream = nullptr;
-        res_owner = false;
-        g_resident_owned[device].store(false);
     }
 };
 thread_local DropInCtx t_ctx;
@@ -1338,13 +1224,16 @@ size_t zero_copy_max() {
     return v;
 }
 
-// Device-usable address for p, or NULL if p is pageable host memory.
-void *device_view(void *p) {
+// Device-usable address for p, or NULL if p is pageable host memory; *host: p is
+// pinned host memory (the kernel reaches it over PCIe).
+void *device_view(void *p, bool *host) {
+    *host = false;
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();
         return nullptr;
     }
+    *host = at.type == hipMemoryTypeHost;
     if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged ||
         at.type == hipMemoryTypeHost)
         return at.devicePointer;
@@ -1390,18 +1279,19 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     const size_t n = static_cast<size_t>(nbytes);
     char *dst = r2 ? r2 : region;
     const int mode_add = r2 ? add : 0;
-    void *vs = device_view(region), *vd = device_view(dst);
+    bool hs = false, hd = false;
+    void *vs = device_view(region, &hs), *vd = device_view(dst, &hd);
     if (vs && vd) {  // device-resident (or pinned/mapped): run in place
-        c.resident_quiesce();
         DROPIN_CHECK(region_launch(dev, vs, multby, n, vd, mode_add, c.stream, true));
         DROPIN_CHECK(stream_wait(c.stream));
         return;
     }
-    if (n <= zero_copy_max()) {  // small pageable call: zero-copy through mapped pinned memory
-        if (c.zc_cap < n) {
-            c.resident_quiesce();  // (the worker addresses the old staging)
+    const size_t n16 = (n + 15) & ~size_t(15);  // the kernel's extent in the staging
+    const bool host_ok = (!vs || hs) && (!vd || hd);  // both reachable by the CPU's memcpy
+    if (host_ok && n <= zero_copy_max()) {  // small host call: zero-copy through mapped pinned memory
+        if (c.zc_cap < n16) {
             map_cache().release(dev, c.zc, 2 * c.zc_cap);
-            c.zc_cap = std::max(n, size_t(64) << 10);
+            c.zc_cap = std::max(n16, size_t(64) << 10);
             c.zc = static_cast<uint8_t *>(map_cache().acquire(dev, 2 * c.zc_cap));
             if (!c.zc) die("galois_w08_region_multiply: mapped staging allocation failed");
             DROPIN_HIP(hipHostGetDevicePointer(&c.zc_dev, c.zc, 0));
@@ -1409,19 +1299,16 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         uint8_t *zs = c.zc, *zd = c.zc + c.zc_cap;
         memcpy(zs, region, n);
         if (mode_add) memcpy(zd, dst, n);
-        if (n <= kResMax && c.resident_ready(dev)) {
-            c.resident_call(multby, n, mode_add);  // no launch: the resident worker
-        } else {
-            c.resident_quiesce();
-            uint8_t *ds = static_cast<uint8_t *>(c.zc_dev), *dd = ds + c.zc_cap;
-            DROPIN_CHECK(region_launch(dev, ds, multby, n, dd, mode_add, c.stream, true));
-            DROPIN_CHECK(stream_wait(c.stream));  // (spinning on hipStreamQuery instead: no gain)
-        }
+        uint8_t *ds = static_cast<uint8_t *>(c.zc_dev), *dd = ds + c.zc_cap;
+        // n16 bytes: whole 16-byte chunks only, no byte scatter over PCIe (the padding's
+        // results are not copied back)
+        DROPIN_CHECK(region_launch(dev, ds, multby, n16, dd, mode_add, c.stream, true));
+        DROPIN_CHECK(stream_wait(c.stream));  // (spinning on hipStreamQuery instead: no gain)
         memcpy(dst, zd, n);
         return;
     }
-    // larger pageable buffers: stage through device memory chunk by chunk
-    c.resident_quiesce();
+    // larger host buffers (or a device operand with a host result): stage through
+    // device memory chunk by chunk
     const size_t want = std::min(n, kStageChunk);
     if (c.cap < want) {
         dev_cache().release(dev, c.dsrc, c.cap);
@@ -1433,11 +1320,11 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     }
     for (size_t o = 0; o < n; o += kStageChunk) {
         const size_t len = std::min(kStageChunk, n - o);
-        DROPIN_HIP(hipMemcpyAsync(c.dsrc, region + o, len, hipMemcpyHostToDevice, c.stream));
+        DROPIN_HIP(hipMemcpyAsync(c.dsrc, region + o, len, hipMemcpyDefault, c.stream));
         if (mode_add)
-            DROPIN_HIP(hipMemcpyAsync(c.ddst, dst + o, len, hipMemcpyHostToDevice, c.stream));
+            DROPIN_HIP(hipMemcpyAsync(c.ddst, dst + o, len, hipMemcpyDefault, c.stream));
         DROPIN_CHECK(region_launch(dev, c.dsrc, multby, len, c.ddst, mode_add, c.stream, true));
-        DROPIN_HIP(hipMemcpyAsync(dst + o, c.ddst, len, hipMemcpyDeviceToHost, c.stream));
+        DROPIN_HIP(hipMemcpyAsync(dst + o, c.ddst, len, hipMemcpyDefault, c.stream));
         DROPIN_HIP(hipStreamSynchronize(c.stream));
     }
 }

@@ -93,8 +93,6 @@ _SIGS = {
     "cec_get_engine": ([], _i),
     "cec_set_waves_per_cu": ([_i], _i),
     "cec_get_waves_per_cu": ([], _i),
-    "cec_set_dropin_resident": ([_i], _i),
-    "cec_get_dropin_resident": ([], _i),
     "cec_plan_create": ([ctypes.POINTER(_vp), ctypes.POINTER(Extent), _i, _vp], _i),
     "cec_plan_destroy": ([_vp], _i),
     "cec_plan_num_extents": ([_vp], _i),
@@ -262,14 +260,6 @@ def get_engine() -> int:
 def set_waves_per_cu(waves: int) -> None:
     _check(lib().cec_set_waves_per_cu(waves))
 
-
-def set_dropin_resident(enable: bool) -> None:
-    """Small pageable drop-in calls through the resident worker (cocytus_ec.h)."""
-    _check(lib().cec_set_dropin_resident(1 if enable else 0))
-
-
-def get_dropin_resident() -> bool:
-    return bool(lib().cec_get_dropin_resident())
 
 
 def get_waves_per_cu() -> int:

@@ -82,15 +82,6 @@ cec_engine cec_get_engine(void);
  * CEC_WAVES_PER_CU environment variable.  A tuning knob: every value is bit-exact. */
 int cec_set_waves_per_cu(int waves_per_cu);
 int cec_get_waves_per_cu(void);
-/* The drop-in galois_w08_region_multiply on pageable buffers of <= 16 KiB through a
- * resident worker (one workgroup that stays on the GPU and takes requests from a mapped
- * pinned mailbox) instead of a kernel launch per call.  It exits after
- * CEC_RESIDENT_IDLE_US (default 1000) without a request or CEC_RESIDENT_LIFE_US (5000)
- * in total and is relaunched on demand; one per device and process, owned by the first
- * calling thread (other threads launch).  Process-wide; initial value from the
- * CEC_DROPIN_RESIDENT environment variable (default 0).  Bit-exact either way. */
-int cec_set_dropin_resident(int enable);
-int cec_get_dropin_resident(void);
 
 /* ---- arena layout in HBM ----
  * The kernels stream every arena at the same offset at once.  Arenas carved from one

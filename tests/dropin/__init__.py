@@ -27,7 +27,7 @@ def build_dropin(out_dir: str) -> str:
     return exe
 
 
-def run_dropin_threads(tmp_path, threads=8, iters=200, env=None) -> str:
+def run_dropin_threads(tmp_path, threads=8, iters=200) -> str:
     exe = os.path.join(str(tmp_path), "dropin_threads")
     subprocess.run(
         [CC, "-O1", "-std=gnu11", "-I", os.path.join(ROOT, "include"),
@@ -35,8 +35,7 @@ def run_dropin_threads(tmp_path, threads=8, iters=200, env=None) -> str:
          f"-Wl,-rpath,{LIBDIR}", *XFLAGS, "-o", exe],
         check=True,
     )
-    r = subprocess.run([exe, str(threads), str(iters)], capture_output=True, text=True, timeout=600,
-                       env={**os.environ, **(env or {})})
+    r = subprocess.run([exe, str(threads), str(iters)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:] + r.stdout
     return r.stdout
 
