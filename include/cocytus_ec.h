@@ -332,7 +332,10 @@ int cec_cache_set_pattern_limit(int entries);      /* default 4096 (CEC_PATTERN_
  * graph (synchronises the current device first). */
 int cec_cache_trim(void);
 
-/* ---- stream / event helpers, so C and ctypes callers need no HIP header ---- */
+/* ---- stream / event helpers, so C and ctypes callers need no HIP header ----
+ * Events are for timing: recorded without the system-scope fence, so waiting on one
+ * does not make results written into host memory visible.  Use cec_stream_synchronize
+ * (or a synchronous call) before reading those. */
 int cec_event_create(void **ev);
 int cec_event_destroy(void *ev);
 int cec_event_record(void *ev, void *stream);
