@@ -7,9 +7,11 @@
  * galois_w08_region_multiply replaces the GF-Complete region multiply behind
  * memcached.c:2681, 5611, 7764, 7918 and recovery.c:91, 123.  It runs the HIP
  * kernel on the GPU: device pointers (hipMalloc / hipHostMalloc / registered) are
- * used in place, pageable host buffers are staged through device memory.  The call
- * is synchronous (result visible on return), re-entrant, and accepts any alignment
- * and any nbytes >= 0.  Like the original it has no error channel: misuse or a HIP
+ * used in place; pageable host buffers up to 256 KiB go through mapped pinned
+ * staging that the kernel reads and writes over PCIe, larger ones are staged through
+ * device memory.  The call is synchronous (the result is visible on return, in host
+ * memory too: a system-scope release precedes the completion signal), re-entrant, and
+ * accepts any alignment and any nbytes >= 0.  Like the original it has no error channel: misuse or a HIP
  * failure prints a message and aborts (there is no CPU fallback).
  */
 #ifndef COCYTUS_EC_GALOIS_H
