@@ -536,6 +536,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
 
 def run_device(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
+
     ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
     r = measure_device(torch, dist, ec, world, rank, args.workload, args)
     # The other device-resident BASELINE configs at the same N, on the same ranks, so the
