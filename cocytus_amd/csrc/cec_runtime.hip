@@ -1019,7 +1019,9 @@ static int stream_wait(hipStream_t s) {
     // workgroups ran on, and the signal kernel's own fence writes back only its XCD's
     // (a 4098-byte drop-in call read back its second tile stale on some boxes).  An
     // event recorded with the system fence makes the command processor write every L2
-    // back before the signal kernel starts.
+    // back before the signal kernel starts.  (Spinning on hipEventQuery of that event
+    // instead of the signal kernel's flag measured the same per call: 12.9-13.7 against
+    // 12.2-13.4 us for 64 B on one box, profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
     HIP_TRY(hipEventRecord(c.fence, s));
     hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
     HIP_TRY(hipGetLastError());
