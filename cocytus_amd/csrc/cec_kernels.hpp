@@ -77,6 +77,12 @@ struct Tile {
 // launch whose patterns use only slots 0 and 1 (region multiply, the drop-in) takes
 // S = 2, and the kernel reads its grid size from here rather than from gridDim /
 // blockDim: those come from the hidden arguments, which add 256 B to every segment.
+// CombineArgsN::flags: every wave ends with a system-scope release (its XCD's L2 written
+// back, its stores complete), for launches whose outputs the host reads on a signal
+// that does not come from the runtime (the synchronous drop-in over host memory).
+// Honoured by the 1 x 1 (region multiply) launches, which select the kSysRel kernel.
+constexpr uint32_t kFlagSysRelease = 1u;
+
 template <int S>
 struct CombineArgsN {
     uint8_t *base[S];
@@ -87,6 +93,7 @@ struct CombineArgsN {
     uint32_t n_tiles;
     uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
     uint32_t grid;         // workgroups in the launch (the grid-stride step)
+    uint32_t flags;        // kFlagSysRelease (fills the struct's padding: same size)
 };
 using CombineArgs = CombineArgsN<kMaxStreams>;
 constexpr int kNarrowStreams = 2;
@@ -258,7 +265,9 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 
 // A workgroup covers 1 / 2^split_shift of a tile (blockDim = kBlock >> split_shift):
 // work item g is tile g >> split_shift, part g & (2^split_shift - 1).
-template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams>
+// kSysRel: every wave ends with a system-scope release (kFlagSysRelease launches; a
+// template parameter, so the batched kernels carry no epilogue at all).
+template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams, bool kSysRel = false>
 __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
     extern __shared__ uint4 cec_lds_rows[];  // LDS engine: the pattern's product rows
     const uint8_t *lds = reinterpret_cast<const uint8_t *>(cec_lds_rows);
@@ -365,6 +374,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
                 if (l < n_out) scatter16(out[l], pos, cnt, acc[l]);
         }
     }
+    if constexpr (kSysRel) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope)
 }
 
 }  // namespace cec

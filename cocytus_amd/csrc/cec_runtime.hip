@@ -143,9 +143,9 @@ static void assign_rows(Pattern &p, std::vector<uint8_t> &rows) {
 
 // ============================================================== launch
 // `lds`: dynamic LDS bytes of the launch (LDS engine: the largest pattern's rows).
-template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams>
+template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams, bool kSysRel = false>
 static void launch_k(const CombineArgsN<S> &a, int grid, size_t lds, hipStream_t s) {
-    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact, S>), dim3(grid),
+    hipLaunchKernelGGL((combine_kernel<NT, LT, Eng, kAcc, kExact, S, kSysRel>), dim3(grid),
                        dim3(kBlock >> a.split_shift), lds, s, a);
 }
 
@@ -162,7 +162,11 @@ static bool launch_narrow(int acc, const CombineArgs &w, int grid, size_t lds, h
     a.n_tiles = w.n_tiles;
     a.split_shift = w.split_shift;
     a.grid = w.grid;
-    if (acc == kAccAll) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams>(a, grid, lds, s);
+    a.flags = w.flags;
+    const bool rel = (w.flags & kFlagSysRelease) != 0;
+    if (acc == kAccAll && rel) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams, true>(a, grid, lds, s);
+    else if (acc == kAccAll) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams>(a, grid, lds, s);
+    else if (acc == kAccNone && rel) launch_k<1, 1, Eng, kAccNone, true, kNarrowStreams, true>(a, grid, lds, s);
     else if (acc == kAccNone) launch_k<1, 1, Eng, kAccNone, true, kNarrowStreams>(a, grid, lds, s);
     else return false;
     return true;
@@ -412,11 +416,14 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 // One launch over n_tiles (> 0) tiles of a plan or an implicit region, with the tables
 // (n_pats patterns, then the LDS engine's rows) already on the device.  The caller
 // checks hipGetLastError.
-static void launch_combine(int dev, const Streams &st, const uint8_t *tables, size_t n_pats,
+// Returns whether kFlagSysRelease (if set) was honoured: only the narrow 1 x 1 launches
+// carry the release epilogue.
+static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, size_t n_pats,
                            const LaunchShape &sh, bool lds, const cec_plan *plan, uint64_t implicit_len,
-                           uint64_t n_tiles, hipStream_t stream) {
+                           uint64_t n_tiles, hipStream_t stream, uint32_t flags = 0) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
+    a.flags = flags;
     for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
     if (plan) a.tiles = plan->d_tiles;
     else a.implicit_len = implicit_len;
@@ -438,7 +445,7 @@ static void launch_combine(int dev, const Streams &st, const uint8_t *tables, si
     if (sh.exact && sh.en == 1 && sh.el == 1 && sh.streams <= kNarrowStreams &&
         (lds ? launch_narrow<LdsEngine>(sh.eacc, a, grid, lds_bytes, stream)
              : launch_narrow<PermEngine>(sh.eacc, a, grid, lds_bytes, stream)))
-        return;
+        return true;
     const bool exact = sh.exact &&
                        (lds ? launch_exact<LdsEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream)
                             : launch_exact<PermEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream));
@@ -446,6 +453,7 @@ static void launch_combine(int dev, const Streams &st, const uint8_t *tables, si
         if (lds) launch_generic<LdsEngine>(sh.nt, sh.lt, a, grid, lds_bytes, stream);
         else launch_generic<PermEngine>(sh.nt, sh.lt, a, grid, lds_bytes, stream);
     }
+    return flags == 0;
 }
 
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
@@ -620,8 +628,9 @@ thread_local RegionMemo t_region;
 }  // namespace
 
 // `plain`: s is known not to be capturing (the drop-in's private stream).
+// flags / *released: see launch_combine (the 1 x 1 region launches honour the release).
 static int region_launch(int dev, const void *src, int multby, size_t n, void *dst, int add, hipStream_t s,
-                         bool plain) {
+                         bool plain, uint32_t flags = 0, bool *released = nullptr) {
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
     if (n_tiles > 0xFFFFFFFFull) return fail(CEC_EINVAL, "region too large");
     const int engine = g_engine.load();
@@ -648,8 +657,9 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
         PatEntry *e = nullptr;
         if (int r = pattern_get(dev, std::move(k), s, &e)) return r;
         if (capturing) {  // tables now marked captured: pinned for this launch only
-            launch_combine(dev, st, e->d, 1, launch_shape(pats, nullptr), engine == CEC_ENGINE_LDS, nullptr, n,
-                           n_tiles, s);
+            const bool rel = launch_combine(dev, st, e->d, 1, launch_shape(pats, nullptr),
+                                            engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s, flags);
+            if (released) *released = rel;
             pattern_done(e);
             HIP_TRY(hipGetLastError());
             return CEC_OK;
@@ -660,7 +670,9 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
         m.e = e;
         m.shape = launch_shape(pats, nullptr);
     }
-    launch_combine(dev, st, m.e->d, 1, m.shape, engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s);
+    const bool rel = launch_combine(dev, st, m.e->d, 1, m.shape, engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s,
+                                    flags);
+    if (released) *released = rel;
     HIP_TRY(hipGetLastError());
     return CEC_OK;
 }
@@ -997,7 +1009,9 @@ thread_local SignalCtx t_signal;
 // (tools/launch_latency.hip, profiles/r01_launch_latency.txt).  After 200 us (a large
 // op, or a kernel that faulted and never signals) it falls back to
 // hipStreamSynchronize, which also reports errors.
-static int stream_wait(hipStream_t s) {
+// `host_results`: the work wrote host memory that the caller reads on return, and its
+// kernels did not end with their own system-scope release (kFlagSysRelease).
+static int stream_wait(hipStream_t s, bool host_results) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     SignalCtx &c = t_signal;
@@ -1017,12 +1031,14 @@ static int stream_wait(hipStream_t s) {
     const uint32_t v = ++c.seq;
     // The op's stores into host memory may still sit in the L2 of the XCDs its
     // workgroups ran on, and the signal kernel's own fence writes back only its XCD's
-    // (a 4098-byte drop-in call read back its second tile stale on some boxes).  An
-    // event recorded with the system fence makes the command processor write every L2
-    // back before the signal kernel starts.  (Spinning on hipEventQuery of that event
-    // instead of the signal kernel's flag measured the same per call: 12.9-13.7 against
-    // 12.2-13.4 us for 64 B on one box, profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
-    HIP_TRY(hipEventRecord(c.fence, s));
+    // (a 4098-byte drop-in call read back its second tile stale on some boxes).  Either
+    // every wave of the op ended with a system-scope release (kFlagSysRelease: the
+    // drop-in), or an event recorded here with the system fence makes the command
+    // processor write every L2 back before the signal kernel starts (4-5 us more per
+    // call on one box, profiles/r02_evidence_s3/fence_cost_ab.jsonl).  (Spinning on
+    // hipEventQuery of that event instead of the signal kernel's flag measured the same
+    // per call: profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
+    if (host_results) HIP_TRY(hipEventRecord(c.fence, s));
     hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
     HIP_TRY(hipGetLastError());
     const auto t0 = std::chrono::steady_clock::now();
@@ -1284,8 +1300,9 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     bool hs = false, hd = false;
     void *vs = device_view(region, &hs), *vd = device_view(dst, &hd);
     if (vs && vd) {  // device-resident (or pinned/mapped): run in place
-        DROPIN_CHECK(region_launch(dev, vs, multby, n, vd, mode_add, c.stream, true));
-        DROPIN_CHECK(stream_wait(c.stream));
+        bool rel = true;  // (a pinned destination: the kernel's waves release it themselves)
+        DROPIN_CHECK(region_launch(dev, vs, multby, n, vd, mode_add, c.stream, true, hd ? kFlagSysRelease : 0, &rel));
+        DROPIN_CHECK(stream_wait(c.stream, !rel));
         return;
     }
     const size_t n16 = (n + 15) & ~size_t(15);  // the kernel's extent in the staging
@@ -1304,8 +1321,9 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         uint8_t *ds = static_cast<uint8_t *>(c.zc_dev), *dd = ds + c.zc_cap;
         // n16 bytes: whole 16-byte chunks only, no byte scatter over PCIe (the padding's
         // results are not copied back)
-        DROPIN_CHECK(region_launch(dev, ds, multby, n16, dd, mode_add, c.stream, true));
-        DROPIN_CHECK(stream_wait(c.stream));  // (spinning on hipStreamQuery instead: no gain)
+        bool rel = false;
+        DROPIN_CHECK(region_launch(dev, ds, multby, n16, dd, mode_add, c.stream, true, kFlagSysRelease, &rel));
+        DROPIN_CHECK(stream_wait(c.stream, !rel));  // (spinning on hipStreamQuery instead: no gain)
         memcpy(dst, zd, n);
         return;
     }
