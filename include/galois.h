@@ -10,7 +10,8 @@
  * used in place; pageable host buffers up to 256 KiB go through mapped pinned
  * staging that the kernel reads and writes over PCIe, larger ones are staged through
  * device memory.  The call is synchronous (the result is visible on return, in host
- * memory too: a system-scope release precedes the completion signal), re-entrant, and
+ * memory too: the kernel's waves release it at system scope before the completion
+ * signal), re-entrant, and
  * accepts any alignment and any nbytes >= 0.  Like the original it has no error channel: misuse or a HIP
  * failure prints a message and aborts (there is no CPU fallback).
  */
