@@ -374,7 +374,12 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
                 if (l < n_out) scatter16(out[l], pos, cnt, acc[l]);
         }
     }
-    if constexpr (kSysRel) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // (system scope)
+    if constexpr (kSysRel) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this XCD's L2 written back
+        // ... and completed before the wave ends (the fence alone leaves the wait to a
+        // following store, and there is none)
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 }
 
 }  // namespace cec
