@@ -86,7 +86,7 @@ def _run_bench(args, env_extra=None, timeout=300):
                           capture_output=True, text=True, timeout=timeout)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_bench_self_launches_ranks(world):
     """`python bench.py --gpus N` with no torch.distributed.run parent (how the driver runs
     it) starts N ranks itself and prints exactly ONE JSON line on stdout (rank 0's), with
