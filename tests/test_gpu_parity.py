@@ -1162,12 +1162,15 @@ def test_recovery_finish_rejects_early_peer(gpu, oracle):
 
 # ------------------------------------------------------------------ recovery pool (§8f 2)
 @pytest.mark.parametrize("engine_name", ["perm", "lds"])
-def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
+@pytest.mark.parametrize("out_kind", ["device", "pinned"])
+def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
     """The idle recoverer's traffic (memcached.c:5712-5734): single-unit and short-range
     requests, a bounded window in flight, replies from D1 / D2 in random order, flushes at
     random points, SETs on D1 / D2 landing mid-recovery (fold_update, then the parity
     apply, memcached.c:7757-7764), batched leader solves.  Every rebuilt unit of lost D0
-    equals the live data."""
+    equals the live data.  With `pinned`, the rebuilt shard's arena is pinned host memory
+    and is read as soon as the last synchronous solve returns (no device sync): the pool
+    then waits with the system-fence event."""
     torch, ec = gpu
     default = ec.get_engine()
     ec.set_engine(ec.CEC_ENGINE_PERM if engine_name == "perm" else ec.CEC_ENGINE_LDS)
@@ -1178,7 +1181,8 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
         nunits = 256
         data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
         p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
-        out0 = torch.zeros(nunits * U, dtype=torch.uint8, device="cuda")
+        out0 = (torch.zeros(nunits * U, dtype=torch.uint8).pin_memory() if out_kind == "pinned"
+                else torch.zeros(nunits * U, dtype=torch.uint8, device="cuda"))
         mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])  # D0 lost, leader P0
         pending, done = {}, []  # id -> (ub, ue, peers left)
         next_unit, window = 0, 24
@@ -1230,6 +1234,8 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name):
                         pool.end(d)
                     done = []
             assert pool.active == 0
+            if out_kind == "pinned":  # read on return of the last synchronous call
+                assert np.array_equal(out0.numpy(), data[0])
         torch.cuda.synchronize()
         assert np.array_equal(to_host(out0), data[0])
     finally:
