@@ -3,7 +3,7 @@
 //
 // Modes (one resident workgroup each, 4 KiB requests, ping-pong from the host):
 //   pull : mailbox + operands in mapped pinned host memory; the worker polls and reads
-//          them over PCIe (what cec_resident.inc does)
+//          them over PCIe (the resident worker of commit 3200187, since removed)
 //   push : mailbox + operands in fine-grained device memory that the host writes through
 //          its mapping; the worker polls and reads HBM, writes the result and the
 //          acknowledgement into mapped pinned host memory
