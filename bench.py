@@ -55,6 +55,8 @@ EXTRA_WORKLOADS = {
                         "data side + 7739-7798 parity side), 65,536 x 4 KiB SETs, device-resident",
     "rs32_e2e": "RS(3,2) 4 KiB encode + decode, values from and back to pinned host memory "
                 "(H2D -> kernels -> D2H pipelined over HIP streams)",
+    "rs32_4k_lds": "the metric's workload with the LDS engine: GF(2^8) products from 256-entry "
+                   "log/antilog product rows staged in LDS (the north star's named kernel form)",
 }
 
 
@@ -75,10 +77,12 @@ def parse(argv=None):
     ap.add_argument("--e2e-zero-copy", action="store_true",
                     help="--e2e with the kernels reading / writing pinned host memory directly")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-strong", action="store_true",
+                    help="skip the fixed-batch (strong scaling) record of the metric's workload")
     ap.add_argument("--harness-check", action="store_true",
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
-    ap.add_argument("--also", default="rs32_mixed,rs32_1m,rs42_64k,rs32_diff_update,rs32_e2e",
+    ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_diff_update,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -175,12 +179,17 @@ def cpu_thread_counts(allowed: int) -> list[int]:
     return sorted({t for t in (1, 16, 64, allowed) if 1 <= t <= allowed})
 
 
-def cpu_baseline(k, m, n, wall_s, threads_list=None):
+CPU_SAMPLES = 5  # timed passes per thread count, after one warm-up pass
+
+
+def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES):
     """Oracle (restated Jerasure/GF-Complete, AVX2) on the host cores, bounded samples.
 
-    One pthread per CPU on disjoint stripes, swept over cpu_thread_counts(); each
-    point runs about wall_s / len(sweep) seconds.  `value` / `cores` is the all-CPU
-    point (the host's ceiling); `reference_config` is the 1-thread point."""
+    One pthread per CPU on disjoint stripes, swept over cpu_thread_counts(); at each
+    point the batch is filled once, one pass warms up, then `samples` timed passes of
+    about wall_s / len(sweep) / (samples + 1) seconds each: median, min and max.
+    `value` / `cores` is the median of the all-CPU point (the host's ceiling);
+    `reference_config` is the 1-thread point (the reference's configuration)."""
     from oracle import pyoracle
 
     h = host_cpu()
@@ -190,28 +199,35 @@ def cpu_baseline(k, m, n, wall_s, threads_list=None):
     counts = threads_list or cpu_thread_counts(allowed)
     per_point = max(0.2, wall_s / len(counts))
     stripes = (256 << 20) // n  # 256 MiB per shard, 1.25 GiB for RS(3,2): above any LLC
+    payload = (k + 1) * n * stripes  # K*n encoded + n rebuilt per stripe, as the GPU metric
     simd = "AVX2" if pyoracle.simd_available() else "scalar"
     sweep = []
     for T in counts:
-        t1 = pyoracle.bench_encode_decode(k, m, n, stripes, T, 1, True)  # calibrate (fill untimed)
-        reps = max(1, min(1000, int(per_point / max(t1, 1e-6))))
-        t = pyoracle.bench_encode_decode(k, m, n, stripes, T, reps, True)
-        sweep.append({"threads": T, "value": round((k + 1) * n * stripes * reps / t / 2**30, 3),
-                      "wall_s": round(t, 2), "passes": reps})
+        # calibrate: one pass after a warm-up pass (fill untimed)
+        t1 = pyoracle.bench_encode_decode_samples(k, m, n, stripes, T, 1, 2, True)[1]
+        reps = max(1, min(1000, int(per_point / (samples + 1) / max(t1, 1e-6))))
+        ts = pyoracle.bench_encode_decode_samples(k, m, n, stripes, T, reps, samples + 1, True)[1:]
+        vals = sorted(round(payload * reps / t / 2**30, 3) for t in ts)
+        sweep.append({"threads": T, "value": statistics.median(vals), "median": statistics.median(vals),
+                      "min": vals[0], "max": vals[-1], "samples": vals, "passes_per_sample": reps,
+                      "wall_s": round(sum(ts), 2)})
     top = sweep[-1]
     from oracle import jerasure_probe
 
     ref_lib, where = jerasure_probe.load()  # probe for the real library
     return {
-        "value": top["value"],
+        "value": top["median"],
         "unit": "GiB/s",
         "cores": top["threads"],
         "host": h,
         "kind": "port",
-        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes, {top['passes']} passes on "
-                  f"{top['threads']} threads ({top['wall_s']:.2f} s wall): every CPU this process may use "
-                  f"(affinity {h['affinity']}, cgroup quota {h['cpu_quota']}), the host's ceiling for it; "
-                  f"restated GF-Complete SPLIT(8,4) split-nibble ({simd}), chained like memcached.c/recovery.c",
+        "label": "restated CPU baseline",  # Jerasure / GF-Complete absent
+        "median": top["median"], "min": top["min"], "max": top["max"], "samples": top["samples"],
+        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes on {top['threads']} threads: "
+                  f"median of {samples} timed passes ({top['passes_per_sample']} repetitions each) after "
+                  f"one warm-up pass; every CPU this process may use (affinity {h['affinity']}, cgroup "
+                  f"quota {h['cpu_quota']}), the host's ceiling for it; restated GF-Complete SPLIT(8,4) "
+                  f"split-nibble ({simd}), chained like memcached.c/recovery.c",
         "reference_config": dict(sweep[0], note="1 thread: the reference's configuration, one worker "
                                                 "thread per server process (memcached.c:6990)"),
         "sweep": sweep,
@@ -256,12 +272,29 @@ def setup(backend="nccl"):
     return torch, dist, ec, world, rank
 
 
-def measure_device(torch, dist, ec, world, rank, workload, args):
+def share_layout(stripes, lo, hi):
+    """Stripes [lo, hi) of a batch, re-based to offset 0 (one GPU's own arenas hold its
+    share of a fixed batch: SURVEY §8e), and the arena bytes they need."""
+    sub = stripes[lo:hi]
+    if not sub:
+        return [], 0
+    base = sub[0][0]
+    out = [(o - base, ln) for o, ln in sub]
+    return out, (out[-1][0] + out[-1][1] + 15) & ~15
+
+
+def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     """Encode + rotating single-shard decode of `workload`, timed over args.steps.
 
+    share = (lo, hi): this rank runs only stripes [lo, hi) of the workload's batch (the
+    fixed-batch split of SURVEY §8e); `value` then counts the whole batch's payload once
+    over all ranks (strong scaling).  Otherwise every rank runs the whole batch (weak).
     Returns the rank-0 result fields (every rank returns them; only rank 0 prints)."""
     k, m, n, _, what = WORKLOADS[workload]
     stripes, arena = layout(workload)
+    full_bytes = sum(ln for _, ln in stripes)
+    if share is not None:
+        stripes, arena = share_layout(stripes, *share)
     B = len(stripes)
     mat = ec.coding_matrix(k, m)
     g = torch.Generator(device="cuda").manual_seed(0xC0C70002 + rank)
@@ -290,18 +323,27 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
     # 2s+1..2s+2 its decode.  (An event before and after every launch cost 1.4 % of the
     # step, two per step 0.4 %: tools/event_cost.py)
     evs = [ec.Event() for _ in range(2 * args.steps + 1)]
+    host = [0.0, 0.0]  # host time spent enqueueing the encodes / the decodes
+    pc = time.perf_counter
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    t0 = pc()
     evs[0].record(stream)
     for s in range(args.steps):
+        h0 = pc()
         ec.encode(k, m, mat, data, parity, enc_plan, stream)
+        h1 = pc()
         evs[2 * s + 1].record(stream)
+        h2 = pc()
         ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
+        h3 = pc()
         evs[2 * s + 2].record(stream)
+        host[0] += h1 - h0
+        host[1] += h3 - h2
+    t_enq = pc() - t0  # the host is this far ahead of the GPU when the loop ends
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0  # this rank's K steps; the max over ranks is taken below
+    elapsed = pc() - t0  # this rank's K steps; the max over ranks is taken below
     if world > 1:
         dist.barrier()
     enc_t = [evs[2 * s].elapsed_ms(evs[2 * s + 1]) for s in range(args.steps)]
@@ -325,7 +367,8 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
     dec_plan.destroy()
     del arenas, data, parity, out
 
-    payload = (k + 1) * bytes_total * world * args.steps
+    # weak: every rank ran the whole batch; strong: the ranks' shares add up to one batch
+    payload = (k + 1) * (full_bytes if share is not None else bytes_total * world) * args.steps
     enc_bytes = (k + m) * bytes_total  # algorithmic HBM bytes per encode launch
     dec_bytes = (k + 1) * bytes_total  # per decode launch (read K survivors, write 1)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
@@ -336,6 +379,10 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
         "value": payload / elapsed / 2**30,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "verified": ok and bad == 0.0,
+        "kernel_ms_per_step": enc_ms + dec_ms,
+        "host_enqueue_us": {"encode": round(host[0] / args.steps * 1e6, 2),
+                            "decode": round(host[1] / args.steps * 1e6, 2),
+                            "step_loop": round(t_enq / args.steps * 1e6, 2)},
         "roofline": {
             "bound": "hbm",
             "achieved": round(enc_gbps, 1),
@@ -355,6 +402,50 @@ def measure_device(torch, dist, ec, world, rank, workload, args):
             "launch_ms_median": round(statistics.median(dec_t), 4), "traffic": dec_traffic,
         },
     }
+
+
+STRONG_PREDICT_N = (2, 4, 8)
+
+
+def measure_strong(torch, dist, ec, world, rank, args, whole):
+    """Fixed-batch (strong) scaling of the metric's workload, SURVEY §8e: the batch's
+    65,536 stripes split contiguously over the ranks with shard_range, each GPU holding
+    only its share; aggregate = whole-batch payload / max over ranks of the step time.
+
+    At N = 1 the shares a fixed batch gives at N = 2, 4, 8 are timed on the one GPU
+    instead (32,768, 16,384, 8,192 stripes): GPUs share nothing on this path (no
+    collective, no host or PCIe traffic in the timed region), so the N-GPU step takes
+    what one GPU takes for its share, and the predicted factor is t(batch) / t(share).
+    `whole` is the weak (whole-batch) result of this rank, the N = 1 point."""
+    B = WORKLOADS[args.workload][3] if WORKLOADS[args.workload][2] else len(layout(args.workload)[0])
+
+    def point(r, stripes, n_gpus):
+        return {"n_gpus": n_gpus, "stripes_per_gpu": stripes, "ms_per_step": round(r["ms_per_step"], 4),
+                "kernel_ms_per_step": round(r["kernel_ms_per_step"], 4),
+                "encode_ms": r["roofline"]["launch_ms"], "decode_ms": r["decode_roofline"]["launch_ms"],
+                "gap_ms_per_step": round(r["ms_per_step"] - r["kernel_ms_per_step"], 4),
+                "host_enqueue_us": r["host_enqueue_us"], "verified": r["verified"]}
+
+    if world > 1:
+        lo, hi = shard_range(B, rank, world)
+        r = measure_device(torch, dist, ec, world, rank, args.workload, args, share=(lo, hi))
+        out = point(r, hi - lo, world)
+        out.update(value=round(r["value"], 2), unit="GiB/s",
+                   split=f"stripes [g*{B}/{world}, (g+1)*{B}/{world}) on GPU g (shard_range), "
+                         "max over ranks")
+        return out
+    t1 = whole["ms_per_step"]
+    pts = [dict(point(whole, B, 1), speedup=1.0, efficiency=1.0, value=round(whole["value"], 2))]
+    for N in STRONG_PREDICT_N:
+        torch.cuda.empty_cache()
+        r = measure_device(torch, dist, ec, 1, 0, args.workload, args, share=(0, B // N))
+        sp = t1 / r["ms_per_step"]
+        pts.append(dict(point(r, B // N, N), speedup=round(sp, 3), efficiency=round(sp / N, 4),
+                        value=round(whole["value"] * sp, 2)))
+    return {"n_gpus": 1, "value": round(whole["value"], 2), "unit": "GiB/s",
+            "predicted": pts,
+            "method": "per-GPU shares of the fixed batch timed on this GPU; predicted value at N = "
+                      "whole-batch payload / the share's step time (no cross-GPU traffic)"}
 
 
 def measure_diff_update(torch, dist, ec, world, rank, args):
@@ -539,6 +630,10 @@ def run_device(args):
 
     ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
     r = measure_device(torch, dist, ec, world, rank, args.workload, args)
+    strong = None
+    if not args.no_strong:
+        torch.cuda.empty_cache()
+        strong = measure_strong(torch, dist, ec, world, rank, args, r)
     # The other device-resident BASELINE configs at the same N, on the same ranks, so the
     # 1/2/4/8-GPU scaling run also covers configs[3] (RS(4,2) 64 KiB, an 8-GPU config)
     # and the north star's 1 MiB values.  `value` stays the metric's workload.
@@ -551,16 +646,27 @@ def run_device(args):
         if w == "rs32_e2e":
             also[w] = measure_e2e(torch, dist, ec, world, rank, args)
             continue
-        o = measure_device(torch, dist, ec, world, rank, w, args)
+        engine = args.engine
+        if w == "rs32_4k_lds":
+            ec.set_engine(ec.CEC_ENGINE_LDS)
+            engine = "lds"
+        try:
+            o = measure_device(torch, dist, ec, world, rank, "rs32_4k" if w == "rs32_4k_lds" else w, args)
+        finally:
+            ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
         also[w] = {
             "value": round(o["value"], 2), "unit": "GiB/s",
             "ms_per_step": round(o["ms_per_step"], 4),
             "workload": f"RS({o['k']},{o['m']}) encode + single-shard decode, "
                         f"{'%d B' % o['n'] if o['n'] else 'mixed 256 B-1 MiB'} values, "
                         f"{o['B']} stripes per GPU ({o['what']})",
+            "engine": engine,
             "encode_frac": o["roofline"]["frac"], "decode_frac": o["decode_roofline"]["frac"],
+            "encode_ms": o["roofline"]["launch_ms"], "decode_ms": o["decode_roofline"]["launch_ms"],
             "verified": o["verified"],
         }
+        if w == "rs32_4k_lds":
+            also[w]["kernel"] = o["roofline"]["kernel"].replace("PermEngine", "LdsEngine")
     if rank == 0:
         k, m, n, B = r["k"], r["m"], r["n"], r["B"]
         res = {
@@ -588,6 +694,10 @@ def run_device(args):
             "decode_roofline": r["decode_roofline"],
             "verified": r["verified"] and all(v["verified"] for v in also.values()),
         }
+        if strong is not None:
+            res["strong"] = strong
+            res["verified"] = res["verified"] and all(
+                p["verified"] for p in strong.get("predicted", [strong]))
         if also:
             res["other_workloads"] = also
         if world == 1 and not args.no_cpu_baseline:

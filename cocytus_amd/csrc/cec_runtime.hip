@@ -1242,8 +1242,9 @@ size_t zero_copy_max() {
     return v;
 }
 
-// Device-usable address for p, or NULL if p is pageable host memory; *host: p is
-// pinned host memory (the kernel reaches it over PCIe).
+// Device-usable address for p, or NULL if p is pageable host memory; *host: the host
+// may read p on return without a copy -- pinned host memory (the kernel reaches it over
+// PCIe) or managed memory -- so a result written there needs the system-scope release.
 void *device_view(void *p, bool *host) {
     *host = false;
     hipPointerAttribute_t at;
@@ -1251,7 +1252,7 @@ void *device_view(void *p, bool *host) {
         (void)hipGetLastError();
         return nullptr;
     }
-    *host = at.type == hipMemoryTypeHost;
+    *host = at.type == hipMemoryTypeHost || at.type == hipMemoryTypeManaged;
     if (at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged ||
         at.type == hipMemoryTypeHost)
         return at.devicePointer;

@@ -16,6 +16,12 @@
  * (/root/reference/const.h:26).  Unaligned offsets and lengths are accepted
  * (slower byte path for the affected tiles), bit-exact either way.
  *
+ * LIFETIME RULE (every object: plan, drainer, recovery session, recovery pool):
+ * destroy the object BEFORE any stream it was used on.  An object records the streams
+ * its calls used and its destroy synchronises exactly those (never the whole device);
+ * a handle of a destroyed stream cannot be synchronised (it crashes the HIP runtime).
+ * This is a change from the first release, whose destroy waited for the whole device.
+ *
  * Coding matrix: int[(k+m)*k], row-major, MATRIX(x,y) = matrix[x*k+y]
  * (/root/reference/memcached.h:52), as returned by
  * reed_sol_big_vandermonde_distribution_matrix(k+m, k, 8)
@@ -101,8 +107,8 @@ int cec_arenas_free(void *slab);
  * stream ordered after it.  Overlapping [off, off+len) ranges are recorded: RMW ops
  * (cec_diff_update, cec_apply_diffs) refuse such a plan with CEC_EOVERLAP. */
 int cec_plan_create(cec_plan **out, const cec_extent *extents, int n, void *stream);
-/* Waits for the streams the plan was used on (its upload and launches; an event
- * recorded on each), never for the device or other streams.  Destroy plans (and
+/* Waits for the streams the plan was used on (its upload and launches), never for the
+ * device or other streams.  LIFETIME RULE (top of this header): destroy plans (and
  * sessions, drainers, pools) before the streams they were used on.  A plan used inside
  * a captured graph must outlive the graph's replays. */
 int cec_plan_destroy(cec_plan *plan);

@@ -79,7 +79,7 @@ void ref_region_multiply_simd(const uint8_t *region, int multby, long nbytes, ui
 
 typedef struct {
     const int *matrix;
-    int k, m, do_decode, reps;
+    int k, m, do_decode, reps, samples;
     long n, s0, s1;
     uint8_t **data, **parity, *out, *res;
     pthread_barrier_t *bar;
@@ -114,6 +114,7 @@ static void *bench_worker(void *p)
     for (int j = 0; j < k; ++j) fill_splitmix(a->data[j], 0xC0C70001ull + (uint64_t)j, lo, hi);
     for (int q = 0; q < m; ++q) memset(a->parity[q] + lo, 0, hi - lo);
     pthread_barrier_wait(a->bar);
+    for (int smp = 0; smp < a->samples; ++smp) {
     for (int r = 0; r < a->reps; ++r) {
         for (long s = a->s0; s < a->s1; ++s) {
             const long off = s * n;
@@ -134,13 +135,19 @@ static void *bench_worker(void *p)
             ref_region_multiply_simd(a->res, inv, n, a->out);
         }
     }
+    pthread_barrier_wait(a->bar);  /* end of sample smp: the main thread timestamps it */
+    }
     return NULL;
 }
 
-double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
-                               int reps, int do_decode)
+/* `samples` timed passes of `reps` repetitions each over the same filled stripes
+ * (one fill, untimed); t[i] = seconds of sample i (CLOCK_MONOTONIC between the
+ * barriers that end consecutive samples: every thread has finished it). */
+int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int threads,
+                                    int reps, int do_decode, int samples, double *t)
 {
     if (threads < 1) threads = 1;
+    if (samples < 1 || !t) return -1;
     int *matrix = ref_big_vandermonde(k + m, k);
     uint8_t *data[32], *parity[32];
     const size_t bytes = (size_t)n * (size_t)nstripes;
@@ -151,27 +158,41 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
     pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
     pthread_t *tid = (pthread_t *)calloc((size_t)threads, sizeof(pthread_t));
     bench_arg *args = (bench_arg *)calloc((size_t)threads, sizeof(bench_arg));
-    for (int t = 0; t < threads; ++t) {
-        bench_arg *a = &args[t];
+    for (int th = 0; th < threads; ++th) {
+        bench_arg *a = &args[th];
         a->matrix = matrix; a->k = k; a->m = m; a->n = n; a->reps = reps; a->do_decode = do_decode;
-        a->s0 = nstripes * t / threads;
-        a->s1 = nstripes * (t + 1) / threads;
+        a->samples = samples;
+        a->s0 = nstripes * th / threads;
+        a->s1 = nstripes * (th + 1) / threads;
         a->data = data; a->parity = parity; a->bar = &bar;
         a->out = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
         a->res = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
-        pthread_create(&tid[t], NULL, bench_worker, a);
+        pthread_create(&tid[th], NULL, bench_worker, a);
     }
     struct timespec t0, t1;
     pthread_barrier_wait(&bar);  /* every worker has filled its stripes */
     clock_gettime(CLOCK_MONOTONIC, &t0);
-    for (int t = 0; t < threads; ++t) pthread_join(tid[t], NULL);
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-    for (int t = 0; t < threads; ++t) { free(args[t].out); free(args[t].res); }
+    for (int smp = 0; smp < samples; ++smp) {
+        pthread_barrier_wait(&bar);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        t[smp] = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        t0 = t1;
+    }
+    for (int th = 0; th < threads; ++th) pthread_join(tid[th], NULL);
+    for (int th = 0; th < threads; ++th) { free(args[th].out); free(args[th].res); }
     for (int j = 0; j < k; ++j) free(data[j]);
     for (int q = 0; q < m; ++q) free(parity[q]);
     free(args); free(tid); free(matrix);
     pthread_barrier_destroy(&bar);
-    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+    return 0;
+}
+
+double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
+                               int reps, int do_decode)
+{
+    double t = 0.0;
+    ref_bench_encode_decode_samples(k, m, n, nstripes, threads, reps, do_decode, 1, &t);
+    return t;
 }
 
 double ref_bench_recover(const uint8_t *parity, const uint8_t *const *peers, const int *coefs,

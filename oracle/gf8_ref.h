@@ -120,6 +120,10 @@ int ref_simd_available(void);
  * decode).  Returns elapsed seconds (CLOCK_MONOTONIC) for `reps` passes.         */
 double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
                                int reps, int do_decode);
+/* The same batch filled once, then `samples` timed passes of `reps` repetitions:
+ * t[i] = seconds of pass i (the first is the caller's warm-up). 0, or -1 on bad args. */
+int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int threads,
+                                    int reps, int do_decode, int samples, double *t);
 
 /* The parity's drain loop as the reference runs it (one thread, memcached.c:4350 ->
  * process_rep_command -> galois_w08_region_multiply(diff, MATRIX(self, lid), n,

@@ -43,6 +43,7 @@ _SIGS = {
     "ref_region_multiply_simd": ([ctypes.c_void_p, _i, _l, ctypes.c_void_p], None),
     "ref_simd_available": ([], _i),
     "ref_bench_encode_decode": ([_i, _i, _l, _l, _i, _i, _i], ctypes.c_double),
+    "ref_bench_encode_decode_samples": ([_i, _i, _l, _l, _i, _i, _i, _i, ctypes.POINTER(ctypes.c_double)], _i),
     "ref_bench_apply": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.c_void_p, _i, ctypes.c_void_p], ctypes.c_double),
     "ref_bench_recover": ([ctypes.c_void_p, _vpp, ctypes.c_void_p, _i, _i, _l, ctypes.c_void_p,
@@ -195,6 +196,14 @@ def simd_available() -> bool:
 
 def bench_encode_decode(k, m, n, nstripes, threads, reps=1, do_decode=True) -> float:
     return lib().ref_bench_encode_decode(k, m, n, nstripes, threads, reps, int(do_decode))
+
+
+def bench_encode_decode_samples(k, m, n, nstripes, threads, reps, samples, do_decode=True) -> list[float]:
+    """Seconds of each of `samples` passes (reps repetitions each) over one filled batch."""
+    t = (ctypes.c_double * samples)()
+    if lib().ref_bench_encode_decode_samples(k, m, n, nstripes, threads, reps, int(do_decode), samples, t):
+        raise ValueError("ref_bench_encode_decode_samples: bad arguments")
+    return list(t)
 
 
 def bench_apply(stage: np.ndarray, soffs, addrs, lens, coefs, parity: np.ndarray) -> float:

@@ -152,8 +152,33 @@ def test_cpu_baseline_small():
 
     cb = bench.cpu_baseline(3, 2, 4096, 0.4, threads_list=[1, 2])
     assert cb["cores"] == 2 and cb["kind"] == "port" and cb["value"] > 0
+    assert cb["label"] == "restated CPU baseline"
     assert cb["reference_config"]["threads"] == 1 and cb["reference_config"]["value"] > 0
     assert [p["threads"] for p in cb["sweep"]] == [1, 2]
+    for p in cb["sweep"]:  # median of >= 5 timed passes after a warm-up, at both points
+        assert len(p["samples"]) == bench.CPU_SAMPLES >= 5
+        assert p["min"] <= p["median"] <= p["max"] and p["value"] == p["median"]
+    assert cb["value"] == cb["median"] == cb["sweep"][-1]["median"]
+
+
+def test_share_layout_rebases_a_contiguous_split():
+    """Each GPU's arenas hold only its share of the fixed batch."""
+    import bench
+
+    s, _ = bench.layout("rs32_4k")
+    for world in (2, 4, 8):
+        tot = 0
+        for r in range(world):
+            lo, hi = bench.shard_range(len(s), r, world)
+            sub, arena = bench.share_layout(s, lo, hi)
+            assert sub[0][0] == 0 and arena == (hi - lo) * 4096
+            assert sub[1] == (4096, 4096)
+            tot += sum(ln for _, ln in sub)
+        assert tot == 65536 * 4096
+    s, _ = bench.layout("rs32_mixed")
+    sub, arena = bench.share_layout(s, 10, 20)
+    assert sub[0][0] == 0 and arena % 16 == 0 and arena >= sub[-1][0] + sub[-1][1]
+    assert [ln for _, ln in sub] == [ln for _, ln in s[10:20]]
 
 
 def test_bench_arguments():
@@ -164,7 +189,9 @@ def test_bench_arguments():
     a = bench.parse([])
     assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "perm")
     assert 1 <= a.steps <= 100 and a.warmup >= 1
-    assert set(a.also.split(",")) == {"rs32_mixed", "rs32_1m", "rs42_64k", "rs32_diff_update", "rs32_e2e"}
+    assert set(a.also.split(",")) == {"rs32_4k_lds", "rs32_mixed", "rs32_1m", "rs42_64k",
+                                      "rs32_diff_update", "rs32_e2e"}
+    assert not a.no_strong
     assert bench.parse(["--also="]).also == ""
     with pytest.raises(SystemExit):
         bench.parse(["--also=rs99"])

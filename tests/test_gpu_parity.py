@@ -638,6 +638,64 @@ def test_dropin_mixed_buffers(gpu, oracle):
         assert np.array_equal(pb.numpy(), exp), ("pinned -> pinned", n)
 
 
+def _hip_lib(ec):
+    """The HIP runtime already mapped into this process (torch's), via ctypes."""
+    import ctypes
+
+    rts = sorted(ec._hip_runtimes())
+    assert len(rts) == 1, rts
+    L = ctypes.CDLL(rts[0])
+    L.hipHostMalloc.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    L.hipHostFree.argtypes = [ctypes.c_void_p]
+    L.hipMallocManaged.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_size_t, ctypes.c_uint]
+    L.hipFree.argtypes = [ctypes.c_void_p]
+    return L
+
+
+HOST_KINDS = {  # hipHostMalloc flags (hip_runtime_api.h)
+    "mapped_coherent": 0x2 | 0x40000000,  # the library's own zero-copy staging
+    "coherent": 0x40000000,
+    "default": 0x0,  # torch's pin_memory
+    "noncoherent": 0x80000000,  # cached in the GPU's L2 on every box
+}
+
+
+@pytest.mark.parametrize("kind", sorted(HOST_KINDS) + ["managed"])
+def test_dropin_host_result_visible_from_every_xcd(gpu, oracle, kind):
+    """Round 2's stale-tile defect, box-independent: a drop-in call whose 65 tiles run on
+    every XCD writes a destination the host reads on return, with no synchronisation.
+    Round 2's completion signal wrote back only its own XCD's L2, which lost tiles only
+    on boxes whose host mappings the L2 caches; non-coherent pinned memory is cached on
+    every box, and managed memory is read by the host in place.  Every
+    writing wave must release its own XCD's L2 (kSysRel) for all of them."""
+    import ctypes
+
+    torch, ec = gpu
+    L = _hip_lib(ec)
+    n = 65 * 4096 - 14  # 65 tiles, the last ragged: workgroups on all 8 XCDs
+    p = ctypes.c_void_p()
+    rc = (L.hipMallocManaged(ctypes.byref(p), n, 1) if kind == "managed"
+          else L.hipHostMalloc(ctypes.byref(p), n, HOST_KINDS[kind]))
+    assert rc == 0 and p.value, (kind, rc)
+    try:
+        dst = np.ctypeslib.as_array((ctypes.c_uint8 * n).from_address(p.value))
+        rng = np.random.default_rng(0x5CA1)
+        for rep in range(24):
+            src = rng.integers(0, 256, n, dtype=np.uint8)
+            dsrc = to_dev(torch, src)
+            torch.cuda.synchronize()
+            dst[:] = rng.integers(0, 256, n, dtype=np.uint8)
+            exp = dst.copy()
+            c = [1, 2, 245, 0x53][rep % 4]
+            oracle.region_multiply(src, c, exp, 1)
+            ec.galois_w08_region_multiply(dsrc, c, n, p.value, 1)
+            bad = np.flatnonzero(dst != exp)  # read on return: no synchronize
+            assert bad.size == 0, (kind, rep, c, bad.size, sorted(set((bad // 4096).tolist()))[:16])
+    finally:
+        torch.cuda.synchronize()
+        (L.hipFree if kind == "managed" else L.hipHostFree)(p)
+
+
 def test_dropin_device_buffers(gpu, oracle):
     torch, ec = gpu
     a = oracle.splitmix_bytes(1, 10000)

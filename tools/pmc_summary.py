@@ -44,7 +44,7 @@ def kernel_rows(path):
         return list(csv.DictReader(f))
 
 
-def main(out, rnd):
+def main(out, rnd, engine="perm"):
     summary, traffic, lines = {}, {}, []
     for w in ALGO:
         stats = one(f"{out}/trace_{w}/**/run_kernel_stats.csv")
@@ -113,10 +113,12 @@ def main(out, rnd):
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-        json.dump(traffic, f, indent=1)
-    md = [f"# rocprofv3 summary ({rnd})", "",
-          "bench.py --steps 10 --warmup 2 per workload (rs32_diff_update: --also=rs32_diff_update, only its",
+    if engine == "perm":  # bench.py's `traffic` is the default (PERM) engine's
+        with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
+            json.dump(traffic, f, indent=1)
+    md = [f"# rocprofv3 summary ({rnd}, engine {engine})", "",
+          f"bench.py --steps 10 --warmup 2 --no-strong --engine {engine} per workload "
+          "(rs32_diff_update: --also=rs32_diff_update, only its",
           "<2, 3, ..., 2> kernel counted); durations from --kernel-trace --stats;",
           "HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB, gfx950 correction), separate --pmc passes.", "",
           "| workload | op | avg us | algorithmic GB/s | frac of 8 TB/s | HBM MiB/launch (PMC) | algorithmic MiB | PMC/algo |",
@@ -131,4 +133,10 @@ def main(out, rnd):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    a = sys.argv[1:]
+    eng = "perm"
+    if "--engine" in a:
+        i = a.index("--engine")
+        eng = a[i + 1]
+        del a[i:i + 2]
+    main(a[0], a[1], eng)

@@ -1,0 +1,147 @@
+// tools/small_batch_probe.hip -- fixed per-launch cost of the streaming kernels at the
+// per-GPU shares a fixed batch gives under strong scaling (not product).
+//
+// The RS(3,2) 4 KiB encode at 8,192 stripes (one GPU's share of 65,536 over 8) takes
+// about 4 us more than 1/8 of the whole batch, the decode about 2 us.  This streams
+// the same shapes as XOR kernels (encode 3 reads / 2 writes, decode 3 reads / 1 write;
+// 64-lane workgroups, 16 B per lane, nt loads) alternating encode / decode back to back
+// like bench.py's step, with an event between launches, at 8,192 / 16,384 / 65,536
+// stripes, for each store policy:
+//   nt      __builtin_nontemporal_store (the library's)
+//   plain   raw buffer store, aux 0
+//   sc1     raw buffer store, aux 16 (write-through: the line leaves the XCD's L2)
+//   sc1nt   raw buffer store, aux 18
+// and prints per size and policy the median encode / decode us and, per policy, the
+// fixed cost a of t(stripes) = a + b * stripes fitted from 8,192 and 65,536.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/small_batch_probe.hip -o tools/small_batch_probe.bin
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                              \
+    do {                                                                   \
+        hipError_t ck_ = (x);                                                \
+        if (ck_ != hipSuccess) {                                           \
+            fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(ck_));         \
+            exit(1);                                                       \
+        }                                                                  \
+    } while (0)
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+#define GL __attribute__((address_space(1)))
+
+struct Args {
+    const uint8_t *r[3];
+    uint8_t *w[2];
+    uint32_t bytes;  // per arena (buffer descriptors' range)
+};
+
+template <int AUX>
+__device__ inline void store16(uint8_t *base, uint32_t bytes, uint32_t off, u32x4 v) {
+    if constexpr (AUX < 0) {
+        __builtin_nontemporal_store(v, (GL u32x4 *)((uintptr_t)base + off));
+    } else {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(v, rs, off, 0, AUX);
+    }
+}
+
+template <int W, int AUX>
+__global__ __launch_bounds__(64) void k_stream(Args a) {
+    const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) acc ^= __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)a.r[i] + off));
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        u32x4 v = acc;
+        v.x ^= j;
+        store16<AUX>(a.w[j], a.bytes, off, v);
+    }
+}
+
+__global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
+    for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull) {
+        uint64_t z = seed + (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        p[i] = z ^ (z >> 31);
+    }
+}
+
+template <int AUX>
+static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps, double fit[2][2]) {
+    const uint32_t sizes[] = {8192, 16384, 65536};
+    for (uint32_t stripes : sizes) {
+        const uint32_t bytes = stripes * 4096u;
+        Args enc{{ar[0], ar[1], ar[2]}, {ar[3], ar[4]}, bytes};
+        Args dec{{ar[1], ar[2], ar[3]}, {ar[5], ar[5]}, bytes};
+        const dim3 grid(stripes * 4);
+        std::vector<hipEvent_t> ev(2 * steps + 1);
+        for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        for (int w = 0; w < 3; ++w) {
+            k_stream<2, AUX><<<grid, 64>>>(enc);
+            k_stream<1, AUX><<<grid, 64>>>(dec);
+        }
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(ev[0], 0));
+        for (int s = 0; s < steps; ++s) {
+            k_stream<2, AUX><<<grid, 64>>>(enc);
+            CK(hipEventRecord(ev[2 * s + 1], 0));
+            k_stream<1, AUX><<<grid, 64>>>(dec);
+            CK(hipEventRecord(ev[2 * s + 2], 0));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<float> te(steps), td(steps);
+        for (int s = 0; s < steps; ++s) {
+            CK(hipEventElapsedTime(&te[s], ev[2 * s], ev[2 * s + 1]));
+            CK(hipEventElapsedTime(&td[s], ev[2 * s + 1], ev[2 * s + 2]));
+        }
+        std::sort(te.begin(), te.end());
+        std::sort(td.begin(), td.end());
+        const double e_us = 1e3 * te[steps / 2], d_us = 1e3 * td[steps / 2];
+        const double e_tbs = 5.0 * bytes / (e_us * 1e-6) / 1e12, d_tbs = 4.0 * bytes / (d_us * 1e-6) / 1e12;
+        printf("{\"policy\": \"%s\", \"stripes\": %u, \"encode_us\": %.2f, \"decode_us\": %.2f, "
+               "\"encode_TBps\": %.3f, \"decode_TBps\": %.3f}\n",
+               name, stripes, e_us, d_us, e_tbs, d_tbs);
+        if (stripes == 8192) { fit[0][0] = e_us; fit[1][0] = d_us; }
+        if (stripes == 65536) { fit[0][1] = e_us; fit[1][1] = d_us; }
+        for (auto &e : ev) CK(hipEventDestroy(e));
+    }
+    // t = a + b * stripes through (8192, t8) and (65536, t64)
+    for (int op = 0; op < 2; ++op) {
+        const double b = (fit[op][1] - fit[op][0]) / (65536.0 - 8192.0), a = fit[op][0] - b * 8192.0;
+        printf("{\"policy\": \"%s\", \"op\": \"%s\", \"fixed_us\": %.2f, \"us_per_1k_stripes\": %.3f, "
+               "\"strong8_efficiency\": %.4f}\n",
+               name, op ? "decode" : "encode", a, b * 1024, fit[op][1] / (8.0 * fit[op][0]));
+    }
+    (void)stride;
+}
+
+int main(int argc, char **argv) {
+    const int steps = argc > 1 ? atoi(argv[1]) : 20;
+    const uint64_t len = 65536ull * 4096;
+    uint64_t stride = (len + 4095) / 4096;
+    if (stride % 2 == 0) ++stride;  // the library's odd-4 KiB arena stride
+    stride *= 4096;
+    uint8_t *slab;
+    CK(hipMalloc(&slab, stride * 6));
+    uint8_t *ar[6];
+    for (int i = 0; i < 6; ++i) {
+        ar[i] = slab + i * stride;
+        k_fill<<<4096, 256>>>((uint64_t *)ar[i], len / 8, 0xC0C70000ull + i);
+    }
+    CK(hipDeviceSynchronize());
+    double fit[2][2];
+    for (int rep = 0; rep < 2; ++rep) {  // two passes: policy order effects show up
+        run<-1>("nt", ar, stride, steps, fit);
+        run<0>("plain", ar, stride, steps, fit);
+        run<16>("sc1", ar, stride, steps, fit);
+        run<18>("sc1nt", ar, stride, steps, fit);
+    }
+    CK(hipFree(slab));
+    return 0;
+}
