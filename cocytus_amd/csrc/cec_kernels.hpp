@@ -82,6 +82,12 @@ struct Tile {
 // that does not come from the runtime (the synchronous drop-in over host memory).
 // Honoured by the 1 x 1 (region multiply) launches, which select the kSysRel kernel.
 constexpr uint32_t kFlagSysRelease = 1u;
+// CombineArgsN::flags: the wide stores write through the XCD's L2 (sc1) instead of
+// non-temporal stores that keep the line there.  The host sets it for launches small
+// enough that what they write is read again from the memory-side cache, or that the
+// dirty lines they would leave in L2 are a visible part of the launch (DESIGN.md §4:
+// the per-GPU shares of strong scaling).
+constexpr uint32_t kFlagWriteThrough = 2u;
 
 template <int S>
 struct CombineArgsN {
@@ -93,7 +99,7 @@ struct CombineArgsN {
     uint32_t n_tiles;
     uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
     uint32_t grid;         // workgroups in the launch (the grid-stride step)
-    uint32_t flags;        // kFlagSysRelease (fills the struct's padding: same size)
+    uint32_t flags;        // kFlagSysRelease | kFlagWriteThrough (fills the struct's padding)
 };
 using CombineArgs = CombineArgsN<kMaxStreams>;
 constexpr int kNarrowStreams = 2;
@@ -125,6 +131,17 @@ __device__ inline void st16(uint8_t *base, uint32_t off, const uint4 &v) {
     w.z = v.z;
     w.w = v.w;
     __builtin_nontemporal_store(w, (CEC_GLOBAL u32x4 *)((uintptr_t)base + off));
+}
+// Write-through (sc1) store of one 16-B chunk at base + off, off < kTile: a buffer store
+// through a descriptor built from the wave-uniform tile base (SGPRs).
+__device__ inline void st16_wt(uint8_t *base, uint32_t off, const uint4 &v) {
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(base, 0, kTile, 0x00020000);
+    u32x4 w;
+    w.x = v.x;
+    w.y = v.y;
+    w.z = v.z;
+    w.w = v.w;
+    __builtin_amdgcn_raw_buffer_store_b128(w, rs, off, 0, 16 /* sc1 */);
 }
 __device__ inline uint32_t ld8(const uint8_t *base, uint32_t off) {
     return *(const CEC_GLOBAL uint8_t *)((uintptr_t)base + off);
@@ -365,9 +382,15 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         }
         compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
         if (wide) {
+            if (a.flags & kFlagWriteThrough) {
 #pragma unroll
-            for (int l = 0; l < LT; ++l)
-                if (l < n_out) st16(out[l], pos, acc[l]);
+                for (int l = 0; l < LT; ++l)
+                    if (l < n_out) st16_wt(out[l], pos, acc[l]);
+            } else {
+#pragma unroll
+                for (int l = 0; l < LT; ++l)
+                    if (l < n_out) st16(out[l], pos, acc[l]);
+            }
         } else {
 #pragma unroll
             for (int l = 0; l < LT; ++l)

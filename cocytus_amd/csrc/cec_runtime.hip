@@ -390,6 +390,33 @@ static size_t occupancy_lds(int dev, uint32_t split_shift) {
     return std::min<size_t>(65536, lds > 256 ? lds - 256 : 0);  // strictly below the boundary
 }
 
+// Store policy of a launch (kFlagWriteThrough).  Write-through (sc1) stores finish the
+// launches of up to 512 MiB of streamed bytes sooner, non-temporal stores the larger
+// ones.  RS(3,2) 4 KiB step, bench.py's strong-scaling shares, 3 processes per policy on
+// one box (profiles/r03_evidence/store_policy_ab/): encode / decode us
+//   8,192 stripes   nt 29.9-31.7 / 23.6-23.9   wt 27.5-28.6 / 22.3-22.6
+//  16,384 stripes   nt 54.0-55.3 / 45.5-45.6   wt 53.4-54.0 / 41.0-41.6
+//  32,768 stripes   nt 105.9-106.2 / 88.1-88.6 wt 112.5-112.7 / 81.1-81.8
+//  65,536 stripes   nt 208.0-212.2 / 178.0-178.3  wt 223.3-224.8 / 184.8-186.1
+// i.e. write-through wins at <= 335 MB (encode) and <= 537 MB (decode) per launch and
+// loses at 671 MB (encode) and above.  Auto: write-through when the launch streams at
+// most g_wt_max_bytes (reads + writes).  CEC_STORE_POLICY=nt|wt|auto and
+// CEC_WT_MAX_BYTES override (measurement).
+enum { kStoreAuto = 0, kStoreNt = 1, kStoreWt = 2 };
+static const int g_store_policy = [] {
+    const char *e = getenv("CEC_STORE_POLICY");
+    if (!e || !*e || !strcmp(e, "auto")) return static_cast<int>(kStoreAuto);
+    return !strcmp(e, "wt") ? static_cast<int>(kStoreWt) : static_cast<int>(kStoreNt);
+}();
+static const uint64_t g_wt_max_bytes = [] {
+    const char *e = getenv("CEC_WT_MAX_BYTES");
+    return e && *e ? strtoull(e, nullptr, 0) : (uint64_t(512) << 20);
+}();
+static bool write_through(uint64_t n_tiles, int streams) {
+    if (g_store_policy != kStoreAuto) return g_store_policy == kStoreWt;
+    return n_tiles * kTile * static_cast<uint64_t>(streams) <= g_wt_max_bytes;
+}
+
 // The kernel a pattern set takes: capacities, LDS rows, and the exact shape if every
 // pattern the launch uses has the same one.
 struct LaunchShape {
@@ -423,7 +450,7 @@ static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, si
                            uint64_t n_tiles, hipStream_t stream, uint32_t flags = 0) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
-    a.flags = flags;
+    a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u);
     for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
     if (plan) a.tiles = plan->d_tiles;
     else a.implicit_len = implicit_len;
