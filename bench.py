@@ -123,6 +123,31 @@ def shard_range(total: int, rank: int, world: int) -> tuple[int, int]:
     return total * rank // world, total * (rank + 1) // world
 
 
+def shard_stripes(stripes, rank: int, world: int) -> tuple[int, int]:
+    """The stripes [lo, hi) of rank `rank` in a contiguous split of a batch over `world`
+    GPUs: by count when every value has one size, by byte count for mixed
+    sizes (each rank's share holds about total / world bytes)."""
+    if len({ln for _, ln in stripes}) <= 1:
+        return shard_range(len(stripes), rank, world)
+    ends, acc = [], 0
+    for _, ln in stripes:
+        acc += ln
+        ends.append(acc)
+
+    def cut(r):  # first stripe whose bytes start at or past r * total / world
+        target = acc * r // world
+        lo, hi = 0, len(ends)
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if ends[mid] <= target:
+                lo = mid + 1
+            else:
+                hi = mid
+        return lo if r else 0
+
+    return (cut(rank), cut(rank + 1) if rank + 1 < world else len(stripes))
+
+
 def max_over_ranks(values, dist):
     """Element-wise max of a list of floats over all ranks (identity when alone)."""
     import torch
@@ -417,7 +442,8 @@ def measure_strong(torch, dist, ec, world, rank, args, whole):
     collective, no host or PCIe traffic in the timed region), so the N-GPU step takes
     what one GPU takes for its share, and the predicted factor is t(batch) / t(share).
     `whole` is the weak (whole-batch) result of this rank, the N = 1 point."""
-    B = WORKLOADS[args.workload][3] if WORKLOADS[args.workload][2] else len(layout(args.workload)[0])
+    stripes = layout(args.workload)[0]
+    B = len(stripes)
 
     def point(r, stripes, n_gpus):
         return {"n_gpus": n_gpus, "stripes_per_gpu": stripes, "ms_per_step": round(r["ms_per_step"], 4),
@@ -427,20 +453,21 @@ def measure_strong(torch, dist, ec, world, rank, args, whole):
                 "host_enqueue_us": r["host_enqueue_us"], "verified": r["verified"]}
 
     if world > 1:
-        lo, hi = shard_range(B, rank, world)
+        lo, hi = shard_stripes(stripes, rank, world)
         r = measure_device(torch, dist, ec, world, rank, args.workload, args, share=(lo, hi))
         out = point(r, hi - lo, world)
         out.update(value=round(r["value"], 2), unit="GiB/s",
-                   split=f"stripes [g*{B}/{world}, (g+1)*{B}/{world}) on GPU g (shard_range), "
-                         "max over ranks")
+                   split=f"contiguous split of the {B} stripes over {world} GPUs (shard_stripes: by "
+                         "count, by bytes for mixed sizes), max over ranks")
         return out
     t1 = whole["ms_per_step"]
     pts = [dict(point(whole, B, 1), speedup=1.0, efficiency=1.0, value=round(whole["value"], 2))]
     for N in STRONG_PREDICT_N:
         torch.cuda.empty_cache()
-        r = measure_device(torch, dist, ec, 1, 0, args.workload, args, share=(0, B // N))
+        lo, hi = shard_stripes(stripes, 0, N)
+        r = measure_device(torch, dist, ec, 1, 0, args.workload, args, share=(lo, hi))
         sp = t1 / r["ms_per_step"]
-        pts.append(dict(point(r, B // N, N), speedup=round(sp, 3), efficiency=round(sp / N, 4),
+        pts.append(dict(point(r, hi - lo, N), speedup=round(sp, 3), efficiency=round(sp / N, 4),
                         value=round(whole["value"] * sp, 2)))
     return {"n_gpus": 1, "value": round(whole["value"], 2), "unit": "GiB/s",
             "predicted": pts,

@@ -161,6 +161,24 @@ def test_cpu_baseline_small():
     assert cb["value"] == cb["median"] == cb["sweep"][-1]["median"]
 
 
+def test_shard_stripes_by_count_and_by_bytes():
+    """contiguous split by stripe count for one value size, by byte count for
+    mixed sizes; the shares tile the batch exactly."""
+    import bench
+
+    s, _ = bench.layout("rs32_4k")
+    assert [bench.shard_stripes(s, r, 8) for r in range(8)] == [bench.shard_range(65536, r, 8) for r in range(8)]
+    s, _ = bench.layout("rs32_mixed")
+    total = sum(ln for _, ln in s)
+    for world in (2, 4, 8):
+        spans = [bench.shard_stripes(s, r, world) for r in range(world)]
+        assert spans[0][0] == 0 and spans[-1][1] == len(s)
+        assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+        for lo, hi in spans:  # each share within one 1 MiB value of total / world
+            got = sum(ln for _, ln in s[lo:hi])
+            assert abs(got - total / world) <= (1 << 20), (world, got, total / world)
+
+
 def test_share_layout_rebases_a_contiguous_split():
     """Each GPU's arenas hold only its share of the fixed batch."""
     import bench

@@ -31,7 +31,14 @@ timeout -k 10 200 tools/launch_latency.bin > "$OUT/launch_latency.txt" 2>&1
 timeout -k 10 200 tools/bench_native.bin 20 3 > "$OUT/bench_native.jsonl" 2>&1
 CEC_NATIVE_DEVICE=0 timeout -k 10 200 tools/bench_native.bin 20 3 2 > "$OUT/bench_native_2threads_one_card.jsonl" 2>&1
 CEC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 > "$OUT/bench_gloo2_one_card.jsonl" 2> "$OUT/bench_gloo2.err"
+# the driver's N: 8 ranks on one card (gloo), the weak line and the fixed-batch split
+CEC_BENCH_WATCHDOG=60 CEC_BENCH_DEVICE=0 timeout -k 10 500 python bench.py --gpus 8 --also= \
+    > "$OUT/bench_gloo8_one_card.jsonl" 2> "$OUT/bench_gloo8.err"
+timeout -k 10 120 tools/xcd_visibility_probe.bin 64 200 > "$OUT/xcd_visibility.jsonl" 2>&1
+timeout -k 10 120 tools/small_batch_probe.bin 20 > "$OUT/small_batch_probe.jsonl" 2>&1
 timeout -k 10 200 python tools/du_probe.py > "$OUT/du_probe.json" 2>/dev/null
 timeout -k 10 200 python tools/decode_probe.py > "$OUT/decode_probe.txt" 2>/dev/null
 [ -n "${EVID_NO_PROF:-}" ] || bash tools/profile_round.sh "$ROUND" > "$OUT/profile.log" 2>&1
+[ -n "${EVID_NO_PROF:-}" ] || PROF_ENGINE=lds PROF_WORKLOADS="rs32_4k rs32_diff_update" \
+    bash tools/profile_round.sh "${ROUND}_lds" > "$OUT/profile_lds.log" 2>&1
 echo done > "$OUT/DONE"
