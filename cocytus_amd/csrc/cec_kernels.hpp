@@ -88,6 +88,19 @@ constexpr uint32_t kFlagSysRelease = 1u;
 // dirty lines they would leave in L2 are a visible part of the launch (DESIGN.md §4:
 // the per-GPU shares of strong scaling).
 constexpr uint32_t kFlagWriteThrough = 2u;
+// CombineArgsN::flags: every pattern of the (exact-shape) launch names the same streams,
+// and the host has put them in order -- base[i] = input i, base[NT + l] = output l --
+// with bit kUniInSrc + i (kUniOutSrc + l) set where the stream is addressed by
+// src_off.  A workgroup's stream addresses then depend on its tile and the kernel
+// arguments only, not on its pattern: its first data loads wait for one scalar load
+// (the tile) instead of three in a row (tile, pattern, argument slot), which is what a
+// small launch's start costs.
+constexpr uint32_t kFlagUniform = 4u;
+// CombineArgsN::flags: the launch has one pattern; every tile uses it whatever its
+// pattern field says (the ops whose extents' pattern is "ignored", cocytus_ec.h).
+constexpr uint32_t kFlagOnePattern = 8u;
+constexpr int kUniInSrc = 8;    // 16 bits: inputs
+constexpr int kUniOutSrc = 24;  // 4 bits: outputs
 
 template <int S>
 struct CombineArgsN {
@@ -99,7 +112,7 @@ struct CombineArgsN {
     uint32_t n_tiles;
     uint32_t split_shift;  // 2^split_shift workgroups of kBlock >> split_shift lanes per tile
     uint32_t grid;         // workgroups in the launch (the grid-stride step)
-    uint32_t flags;        // kFlagSysRelease | kFlagWriteThrough (fills the struct's padding)
+    uint32_t flags;        // kFlag* bits (fills the struct's padding)
 };
 using CombineArgs = CombineArgsN<kMaxStreams>;
 constexpr int kNarrowStreams = 2;
@@ -300,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         const uint32_t part = static_cast<uint32_t>(g) & ((1u << sh) - 1u);
         const uint32_t lane = (part << (kBlockLog2 - sh)) + threadIdx.x;
         const TileRef tr = load_tile(a, t);
-        const CEC_CONST Pattern *P = as_const(a.patterns) + tr.pattern;
+        const CEC_CONST Pattern *P = as_const(a.patterns) + ((a.flags & kFlagOnePattern) ? 0u : tr.pattern);
         const int n_in = kExact ? NT : P->n_in;
         const int n_out = kExact ? LT : P->n_out;
         if (!kExact && n_out == 0) continue;
@@ -318,11 +331,13 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         const uint8_t *in[NT];
         uint8_t *out[LT];
         uint64_t mis = 0;
+        const bool uni = kExact && (a.flags & kFlagUniform);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             in[i] = nullptr;
             if (i < n_in) {
-                in[i] = a.base[P->in_stream[i]] + (P->in_src[i] ? tr.src_off : tr.off);
+                if (uni) in[i] = a.base[i] + ((a.flags >> (kUniInSrc + i)) & 1u ? tr.src_off : tr.off);
+                else in[i] = a.base[P->in_stream[i]] + (P->in_src[i] ? tr.src_off : tr.off);
                 mis |= reinterpret_cast<uint64_t>(in[i]);
             }
         }
@@ -330,7 +345,8 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         for (int l = 0; l < LT; ++l) {
             out[l] = nullptr;
             if (l < n_out) {
-                out[l] = a.base[P->out_stream[l]] + (P->out_src[l] ? tr.src_off : tr.off);
+                if (uni) out[l] = a.base[NT + l] + ((a.flags >> (kUniOutSrc + l)) & 1u ? tr.src_off : tr.off);
+                else out[l] = a.base[P->out_stream[l]] + (P->out_src[l] ? tr.src_off : tr.off);
                 mis |= reinterpret_cast<uint64_t>(out[l]);
             }
         }

@@ -280,7 +280,7 @@ struct cec_plan {
     int64_t n_line_tiles = 0;   // full kTile tiles at a 128-B aligned arena offset
     Tile *d_tiles = nullptr;    // from dev_cache() (owned plans only; views borrow)
     bool owned = false;
-    std::vector<cec_extent> h_ext;  // validation of per-op pattern indices
+    uint32_t max_pattern = 0;       // largest extent pattern (per-op index validation)
     std::vector<Tile> h_tiles;      // kept alive for the async upload
     mutable Tracker uses;           // the streams of the tile upload and of every launch
 };
@@ -305,7 +305,7 @@ CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *
     if (!p) return fail(CEC_ENOMEM, "cec_plan_create: host allocation");
     p->device = dev;
     p->n_ext = n;
-    p->h_ext.assign(ext, ext + n);
+    for (int e = 0; e < n; ++e) p->max_pattern = std::max(p->max_pattern, ext[e].pattern);
     size_t total_tiles = 0;
     for (int e = 0; e < n; ++e) total_tiles += tiles_of(ext[e].off, ext[e].len);
     p->h_tiles.resize(total_tiles);
@@ -424,6 +424,11 @@ struct LaunchShape {
     bool exact = false;
     int en = 0, el = 0, eacc = 0;
     int streams = 0;  // 1 + the highest stream slot a used pattern names
+    // exact shape and every used pattern names the same streams (kFlagUniform): their
+    // slots in order, and the kUniInSrc / kUniOutSrc bits
+    bool uniform = false;
+    uint8_t uin[kPatN] = {}, uout[kPatL] = {};
+    uint32_t src_bits = 0;
 };
 
 static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vector<char> *used) {
@@ -437,6 +442,35 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
         for (int j = 0; j < pats[i].n_out; ++j) sh.streams = std::max(sh.streams, pats[i].out_stream[j] + 1);
     }
     sh.exact = exact_shape(pats, used, &sh.en, &sh.el, &sh.eacc);
+    if (sh.exact) {
+        const Pattern *p0 = nullptr;
+        sh.uniform = true;
+        for (size_t i = 0; i < pats.size() && sh.uniform; ++i) {
+            if (used && !(*used)[i]) continue;
+            const Pattern &p = pats[i];
+            if (!p0) {
+                p0 = &p;
+                continue;
+            }
+            for (int j = 0; j < p.n_in; ++j)
+                sh.uniform &= p.in_stream[j] == p0->in_stream[j] && p.in_src[j] == p0->in_src[j];
+            for (int l = 0; l < p.n_out; ++l)
+                sh.uniform &= p.out_stream[l] == p0->out_stream[l] && p.out_src[l] == p0->out_src[l];
+        }
+        if (sh.uniform && p0) {
+            for (int j = 0; j < p0->n_in; ++j) {
+                sh.uin[j] = static_cast<uint8_t>(p0->in_stream[j]);
+                if (p0->in_src[j]) sh.src_bits |= 1u << (kUniInSrc + j);
+            }
+            for (int l = 0; l < p0->n_out; ++l) {
+                sh.uout[l] = static_cast<uint8_t>(p0->out_stream[l]);
+                if (p0->out_src[l]) sh.src_bits |= 1u << (kUniOutSrc + l);
+            }
+            sh.streams = sh.en + sh.el;  // the launch's slots after reordering
+        } else {
+            sh.uniform = false;
+        }
+    }
     return sh;
 }
 
@@ -450,8 +484,16 @@ static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, si
                            uint64_t n_tiles, hipStream_t stream, uint32_t flags = 0) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
-    a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u);
-    for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
+    a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u) |
+              (n_pats == 1 ? kFlagOnePattern : 0u);
+    if (sh.uniform) {
+        // the streams in pattern order: inputs at 0.., outputs at en.. (kFlagUniform)
+        for (int i = 0; i < sh.en; ++i) a.base[i] = st.base[sh.uin[i]];
+        for (int l = 0; l < sh.el; ++l) a.base[sh.en + l] = st.base[sh.uout[l]];
+        a.flags |= kFlagUniform | sh.src_bits;
+    } else {
+        for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
+    }
     if (plan) a.tiles = plan->d_tiles;
     else a.implicit_len = implicit_len;
     a.patterns = reinterpret_cast<const Pattern *>(tables);
@@ -762,6 +804,8 @@ CEC_API int cec_diff_update(int k, int m, const int *matrix, uint8_t *const *dat
     if (int r = check_code(k, m, matrix)) return r;
     if (!plan || !data || !staging || !parity) return fail(CEC_EINVAL, "cec_diff_update: NULL arg");
     if (plan->overlap) return fail(CEC_EOVERLAP, "cec_diff_update: plan extents overlap");
+    if (plan->n_ext && plan->max_pattern >= static_cast<uint32_t>(k))
+        return fail(CEC_EINVAL, "cec_diff_update: an extent names source shard %u (k = %d)", plan->max_pattern, k);
     int dev;
     if (int r = current_device(&dev)) return r;
     Streams st;
@@ -802,6 +846,8 @@ CEC_API int cec_set_diff(int k, const uint8_t *const *data, const uint8_t *stagi
                          const cec_plan *plan, void *stream) {
     if (k < 1 || k > CEC_MAX_K || !plan || !data || !staging || !diff)
         return fail(CEC_EINVAL, "cec_set_diff: bad args");
+    if (plan->n_ext && plan->max_pattern >= static_cast<uint32_t>(k))
+        return fail(CEC_EINVAL, "cec_set_diff: an extent names source shard %u (k = %d)", plan->max_pattern, k);
     int dev;
     if (int r = current_device(&dev)) return r;
     Streams st;
@@ -834,6 +880,8 @@ CEC_API int cec_apply_diffs(int k, int m, const int *matrix, int lid_self, const
     if (lid_self < k || lid_self >= k + m || !diffs || !parity || !plan)
         return fail(CEC_EINVAL, "cec_apply_diffs: bad args (lid_self=%d)", lid_self);
     if (plan->overlap) return fail(CEC_EOVERLAP, "cec_apply_diffs: plan extents overlap");
+    if (plan->n_ext && plan->max_pattern >= static_cast<uint32_t>(k))
+        return fail(CEC_EINVAL, "cec_apply_diffs: an extent names source shard %u (k = %d)", plan->max_pattern, k);
     int dev;
     if (int r = current_device(&dev)) return r;
     Streams st;
@@ -949,10 +997,8 @@ CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, i
         return fail(CEC_EINVAL, "cec_decode: bad args");
     int dev;
     if (int r = current_device(&dev)) return r;
-    for (int e = 0; e < plan->n_ext; ++e)
-        if (plan->h_ext[e].pattern >= static_cast<uint32_t>(n_masks))
-            return fail(CEC_EINVAL, "cec_decode: extent %d names mask %u of %d", e,
-                        plan->h_ext[e].pattern, n_masks);
+    if (plan->n_ext && plan->max_pattern >= static_cast<uint32_t>(n_masks))
+        return fail(CEC_EINVAL, "cec_decode: an extent names mask %u of %d", plan->max_pattern, n_masks);
     Streams st;
     for (int lid = 0; lid < k + m; ++lid) st.base[lid] = const_cast<uint8_t *>(arenas[lid]);
     for (int j = 0; j < k; ++j) st.base[k + m + j] = out[j];
@@ -1033,7 +1079,7 @@ thread_local SignalCtx t_signal;
 // their latency (the per-call drop-in, per-SET recovery folds).  A one-lane kernel
 // writes a sequence number into mapped pinned memory behind the work and the host
 // spins on it: 6.3 us per empty call against 10.5 us for hipStreamSynchronize
-// (tools/launch_latency.hip, profiles/r01_launch_latency.txt).  After 200 us (a large
+// (tools/launch_latency.hip, archive/profiles/r01_launch_latency.txt).  After 200 us (a large
 // op, or a kernel that faulted and never signals) it falls back to
 // hipStreamSynchronize, which also reports errors.
 // `host_results`: the work wrote host memory that the caller reads on return, and its
@@ -1062,9 +1108,9 @@ static int stream_wait(hipStream_t s, bool host_results) {
     // every wave of the op ended with a system-scope release (kFlagSysRelease: the
     // drop-in), or an event recorded here with the system fence makes the command
     // processor write every L2 back before the signal kernel starts (4-5 us more per
-    // call on one box, profiles/r02_evidence_s3/fence_cost_ab.jsonl).  (Spinning on
+    // call on one box, archive/profiles/r02_evidence_s3/fence_cost_ab.jsonl).  (Spinning on
     // hipEventQuery of that event instead of the signal kernel's flag measured the same
-    // per call: profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
+    // per call: archive/profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
     if (host_results) HIP_TRY(hipEventRecord(c.fence, s));
     hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
     HIP_TRY(hipGetLastError());

@@ -56,9 +56,11 @@ typedef enum cec_status {
 /* One value of a batch.  `off` addresses the arenas (item->addr, memcached.h:441);
  * `src_off` addresses the staging buffer that carries values from / to the network
  * (c->vbuf, e->vbuf: memcached.c:3646-3655, 7727-7735); `pattern` is per-op:
- *   cec_diff_update / cec_apply_diffs : source data shard lid j (0..k-1)
+ *   cec_diff_update / cec_apply_diffs /
+ *   cec_set_diff                       : source data shard lid j (0..k-1)
  *   cec_decode                         : index into the op's mask array
- *   other ops                          : ignored (0). */
+ *   other ops                          : ignored (any value).
+ * An index out of range (j >= k, or >= n_masks) makes the op return CEC_EINVAL. */
 typedef struct cec_extent {
     uint64_t off;
     uint64_t src_off;

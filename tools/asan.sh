@@ -32,7 +32,7 @@ run)
   # has unloaded at exit.  With the default 256 MiB, the runtime's own teardown frees
   # can recycle a device-memory chunk that the exit hook freed. ASan's device allocator
   # then fails its CHECK "!dev_runtime_unloaded_" (sanitizer_allocator_device.h:125),
-  # on some boxes and runs and not others (profiles/r02_evidence_final/asan_*).
+  # on some boxes and runs and not others (archive/profiles/r02_evidence_final/asan_*).
   # A larger quarantine only delays reuse, so use-after-free detection gets stronger.
   export ASAN_OPTIONS=detect_leaks=1:abort_on_error=0:verify_asan_link_order=0:quarantine_size_mb=4096
   export LSAN_OPTIONS=suppressions=$R/tools/asan_lsan.supp:print_suppressions=0
