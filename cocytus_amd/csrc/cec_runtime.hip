@@ -193,6 +193,14 @@ static bool launch_exact(int n, int l, int acc, const CombineArgs &a, int grid, 
     return false;
 }
 
+// The (n_in, n_out, acc) shapes launch_exact instantiates.
+static bool has_exact(int n, int l, int acc) {
+    if (acc == kAccNone) return n >= 1 && n <= 8 && l >= 1 && l <= 4;
+    if (acc == kAccAll) return (n == 1 && l == 1) || (n == 2 && l >= 1 && l <= 4);
+    if (acc == kAccAllButLast) return n == 2 && l >= 2 && l <= 4;
+    return false;
+}
+
 // Capacity kernels for every other shape (guarded, per-pattern counts and modes).
 template <class Eng>
 static void launch_generic(int nt, int lt, const CombineArgs &a, int grid, size_t lds, hipStream_t s) {
@@ -442,7 +450,7 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
         for (int j = 0; j < pats[i].n_out; ++j) sh.streams = std::max(sh.streams, pats[i].out_stream[j] + 1);
     }
     sh.exact = exact_shape(pats, used, &sh.en, &sh.el, &sh.eacc);
-    if (sh.exact) {
+    if (sh.exact && has_exact(sh.en, sh.el, sh.eacc)) {  // (kFlagUniform: exact kernels only)
         const Pattern *p0 = nullptr;
         sh.uniform = true;
         for (size_t i = 0; i < pats.size() && sh.uniform; ++i) {
@@ -477,16 +485,53 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 // One launch over n_tiles (> 0) tiles of a plan or an implicit region, with the tables
 // (n_pats patterns, then the LDS engine's rows) already on the device.  The caller
 // checks hipGetLastError.
-// Returns whether kFlagSysRelease (if set) was honoured: only the narrow 1 x 1 launches
-// carry the release epilogue.
-static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, size_t n_pats,
-                           const LaunchShape &sh, bool lds, const cec_plan *plan, uint64_t implicit_len,
-                           uint64_t n_tiles, hipStream_t stream, uint32_t flags = 0) {
+// *released: whether kFlagSysRelease (if set) was honoured (only the narrow 1 x 1 launches
+// carry the release epilogue).  hpats / used: the host copies of the launch's patterns and
+// which of them its tiles name (NULL: all), for the stream check below.
+enum KernelKind { kKindNarrow, kKindExact, kKindGeneric };
+
+// Every stream a kernel of `kind` will dereference for each used pattern, read from the
+// argument layout it will see (kFlagUniform order or pattern slots), is the stream the
+// pattern names, and is not NULL.  A mismatch is a library bug that would fault the GPU:
+// refuse the launch instead.
+static bool stream_layout_ok(const CombineArgs &a, KernelKind kind, const Streams &st, const Pattern *hpats,
+                             size_t n_pats, const std::vector<char> *used) {
+    const bool uni = kind != kKindGeneric && (a.flags & kFlagUniform);
+    const int slots = kind == kKindNarrow ? kNarrowStreams : kMaxStreams;
+    for (size_t q = 0; q < n_pats; ++q) {
+        if (used && (q >= used->size() || !(*used)[q])) continue;
+        if (!used && (a.flags & kFlagOnePattern) && q > 0) break;
+        const Pattern &p = hpats[q];
+        for (int i = 0; i < p.n_in; ++i) {
+            const int slot = uni ? i : p.in_stream[i];
+            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[p.in_stream[i]]) return false;
+        }
+        for (int l = 0; l < p.n_out; ++l) {
+            const int slot = uni ? p.n_in + l : p.out_stream[l];
+            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[p.out_stream[l]]) return false;
+        }
+    }
+    return true;
+}
+
+static int launch_combine(int dev, const Streams &st, const uint8_t *tables, size_t n_pats,
+                          const LaunchShape &sh, bool lds, const cec_plan *plan, uint64_t implicit_len,
+                          uint64_t n_tiles, hipStream_t stream, const Pattern *hpats,
+                          const std::vector<char> *used, uint32_t flags = 0, bool *released = nullptr) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
     a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u) |
               (n_pats == 1 ? kFlagOnePattern : 0u);
-    if (sh.uniform) {
+    // Which kernel runs: the stream order of kFlagUniform is read by the exact-shape
+    // kernels only; a shape without one (e.g. 16 inputs) keeps the slot layout its
+    // patterns name.  (sh.streams counts the reordered slots when uniform.)
+    const bool exact_k = sh.exact && has_exact(sh.en, sh.el, sh.eacc);
+    const KernelKind kind =
+        exact_k && sh.en == 1 && sh.el == 1 && sh.streams <= kNarrowStreams &&
+                (sh.eacc == kAccAll || sh.eacc == kAccNone)
+            ? kKindNarrow
+            : exact_k ? kKindExact : kKindGeneric;
+    if (sh.uniform && kind != kKindGeneric) {
         // the streams in pattern order: inputs at 0.., outputs at en.. (kFlagUniform)
         for (int i = 0; i < sh.en; ++i) a.base[i] = st.base[sh.uin[i]];
         for (int l = 0; l < sh.el; ++l) a.base[sh.en + l] = st.base[sh.uout[l]];
@@ -494,6 +539,9 @@ static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, si
     } else {
         for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
     }
+    if (!stream_layout_ok(a, kind, st, hpats, n_pats, used))
+        return fail(CEC_EINVAL, "internal: a launch's stream layout does not match its patterns "
+                                "(kind %d, %d x %d); not launched", static_cast<int>(kind), sh.en, sh.el);
     if (plan) a.tiles = plan->d_tiles;
     else a.implicit_len = implicit_len;
     a.patterns = reinterpret_cast<const Pattern *>(tables);
@@ -511,18 +559,22 @@ static bool launch_combine(int dev, const Streams &st, const uint8_t *tables, si
     const uint64_t max_wgs = 0xFFFFFFFFull / (kBlock >> a.split_shift);
     const int grid = static_cast<int>(std::min<uint64_t>(n_tiles << a.split_shift, max_wgs));
     a.grid = static_cast<uint32_t>(grid);
-    if (sh.exact && sh.en == 1 && sh.el == 1 && sh.streams <= kNarrowStreams &&
-        (lds ? launch_narrow<LdsEngine>(sh.eacc, a, grid, lds_bytes, stream)
-             : launch_narrow<PermEngine>(sh.eacc, a, grid, lds_bytes, stream)))
-        return true;
-    const bool exact = sh.exact &&
-                       (lds ? launch_exact<LdsEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream)
-                            : launch_exact<PermEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream));
-    if (!exact) {
+    bool ok;
+    if (kind == kKindNarrow) {
+        ok = lds ? launch_narrow<LdsEngine>(sh.eacc, a, grid, lds_bytes, stream)
+                 : launch_narrow<PermEngine>(sh.eacc, a, grid, lds_bytes, stream);
+    } else if (kind == kKindExact) {
+        ok = lds ? launch_exact<LdsEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream)
+                 : launch_exact<PermEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream);
+    } else {
         if (lds) launch_generic<LdsEngine>(sh.nt, sh.lt, a, grid, lds_bytes, stream);
         else launch_generic<PermEngine>(sh.nt, sh.lt, a, grid, lds_bytes, stream);
+        ok = true;
     }
-    return flags == 0;
+    if (!ok) return fail(CEC_EINVAL, "internal: no %s kernel for %d x %d", kind == kKindNarrow ? "narrow" : "exact",
+                         sh.en, sh.el);
+    if (released) *released = kind == kKindNarrow || (flags & kFlagSysRelease) == 0;
+    return CEC_OK;
 }
 
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
@@ -546,12 +598,13 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
     PatEntry *entry = nullptr;
     if (int r = pattern_get(dev, std::move(key), stream, &entry)) return r;
-    launch_combine(dev, st, entry->d, pats.size(), sh, g_engine.load() == CEC_ENGINE_LDS, plan, implicit_len,
-                   n_tiles, stream);
+    const int rc = launch_combine(dev, st, entry->d, pats.size(), sh, g_engine.load() == CEC_ENGINE_LDS, plan,
+                                  implicit_len, n_tiles, stream, pats.data(), used);
     // the plan's streams, for its destroy (host-side only); the tables may be evicted
     // again once the launch is enqueued (eviction synchronises the device)
     if (plan) plan->uses.note(stream);
     pattern_done(entry);
+    if (rc) return rc;
     HIP_TRY(hipGetLastError());
     return CEC_OK;
 }
@@ -689,6 +742,7 @@ struct RegionMemo {
     int dev = -1, key = -1;
     PatEntry *e = nullptr;  // pinned while memoised
     LaunchShape shape;
+    Pattern pat;            // the host copy (launch_combine's stream check)
     ~RegionMemo() {
         if (e) pattern_done(e);
     }
@@ -726,10 +780,10 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
         PatEntry *e = nullptr;
         if (int r = pattern_get(dev, std::move(k), s, &e)) return r;
         if (capturing) {  // tables now marked captured: pinned for this launch only
-            const bool rel = launch_combine(dev, st, e->d, 1, launch_shape(pats, nullptr),
-                                            engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s, flags);
-            if (released) *released = rel;
+            const int rc = launch_combine(dev, st, e->d, 1, launch_shape(pats, nullptr), engine == CEC_ENGINE_LDS,
+                                          nullptr, n, n_tiles, s, pats.data(), nullptr, flags, released);
             pattern_done(e);
+            if (rc) return rc;
             HIP_TRY(hipGetLastError());
             return CEC_OK;
         }
@@ -738,10 +792,11 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
         m.key = key;
         m.e = e;
         m.shape = launch_shape(pats, nullptr);
+        m.pat = pats[0];
     }
-    const bool rel = launch_combine(dev, st, m.e->d, 1, m.shape, engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s,
-                                    flags);
-    if (released) *released = rel;
+    if (int rc = launch_combine(dev, st, m.e->d, 1, m.shape, engine == CEC_ENGINE_LDS, nullptr, n, n_tiles, s,
+                                &m.pat, nullptr, flags, released))
+        return rc;
     HIP_TRY(hipGetLastError());
     return CEC_OK;
 }
