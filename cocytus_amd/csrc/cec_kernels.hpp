@@ -88,19 +88,9 @@ constexpr uint32_t kFlagSysRelease = 1u;
 // dirty lines they would leave in L2 are a visible part of the launch (DESIGN.md §4:
 // the per-GPU shares of strong scaling).
 constexpr uint32_t kFlagWriteThrough = 2u;
-// CombineArgsN::flags: every pattern of the (exact-shape) launch names the same streams,
-// and the host has put them in order -- base[i] = input i, base[NT + l] = output l --
-// with bit kUniInSrc + i (kUniOutSrc + l) set where the stream is addressed by
-// src_off.  A workgroup's stream addresses then depend on its tile and the kernel
-// arguments only, not on its pattern: its first data loads wait for one scalar load
-// (the tile) instead of three in a row (tile, pattern, argument slot), which is what a
-// small launch's start costs.
-constexpr uint32_t kFlagUniform = 4u;
 // CombineArgsN::flags: the launch has one pattern; every tile uses it whatever its
 // pattern field says (the ops whose extents' pattern is "ignored", cocytus_ec.h).
-constexpr uint32_t kFlagOnePattern = 8u;
-constexpr int kUniInSrc = 8;    // 16 bits: inputs
-constexpr int kUniOutSrc = 24;  // 4 bits: outputs
+constexpr uint32_t kFlagOnePattern = 4u;
 
 template <int S>
 struct CombineArgsN {
@@ -331,13 +321,11 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         const uint8_t *in[NT];
         uint8_t *out[LT];
         uint64_t mis = 0;
-        const bool uni = kExact && (a.flags & kFlagUniform);
 #pragma unroll
         for (int i = 0; i < NT; ++i) {
             in[i] = nullptr;
             if (i < n_in) {
-                if (uni) in[i] = a.base[i] + ((a.flags >> (kUniInSrc + i)) & 1u ? tr.src_off : tr.off);
-                else in[i] = a.base[P->in_stream[i]] + (P->in_src[i] ? tr.src_off : tr.off);
+                in[i] = a.base[P->in_stream[i]] + (P->in_src[i] ? tr.src_off : tr.off);
                 mis |= reinterpret_cast<uint64_t>(in[i]);
             }
         }
@@ -345,8 +333,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         for (int l = 0; l < LT; ++l) {
             out[l] = nullptr;
             if (l < n_out) {
-                if (uni) out[l] = a.base[NT + l] + ((a.flags >> (kUniOutSrc + l)) & 1u ? tr.src_off : tr.off);
-                else out[l] = a.base[P->out_stream[l]] + (P->out_src[l] ? tr.src_off : tr.off);
+                out[l] = a.base[P->out_stream[l]] + (P->out_src[l] ? tr.src_off : tr.off);
                 mis |= reinterpret_cast<uint64_t>(out[l]);
             }
         }

@@ -432,11 +432,6 @@ struct LaunchShape {
     bool exact = false;
     int en = 0, el = 0, eacc = 0;
     int streams = 0;  // 1 + the highest stream slot a used pattern names
-    // exact shape and every used pattern names the same streams (kFlagUniform): their
-    // slots in order, and the kUniInSrc / kUniOutSrc bits
-    bool uniform = false;
-    uint8_t uin[kPatN] = {}, uout[kPatL] = {};
-    uint32_t src_bits = 0;
 };
 
 static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vector<char> *used) {
@@ -450,35 +445,6 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
         for (int j = 0; j < pats[i].n_out; ++j) sh.streams = std::max(sh.streams, pats[i].out_stream[j] + 1);
     }
     sh.exact = exact_shape(pats, used, &sh.en, &sh.el, &sh.eacc);
-    if (sh.exact && has_exact(sh.en, sh.el, sh.eacc)) {  // (kFlagUniform: exact kernels only)
-        const Pattern *p0 = nullptr;
-        sh.uniform = true;
-        for (size_t i = 0; i < pats.size() && sh.uniform; ++i) {
-            if (used && !(*used)[i]) continue;
-            const Pattern &p = pats[i];
-            if (!p0) {
-                p0 = &p;
-                continue;
-            }
-            for (int j = 0; j < p.n_in; ++j)
-                sh.uniform &= p.in_stream[j] == p0->in_stream[j] && p.in_src[j] == p0->in_src[j];
-            for (int l = 0; l < p.n_out; ++l)
-                sh.uniform &= p.out_stream[l] == p0->out_stream[l] && p.out_src[l] == p0->out_src[l];
-        }
-        if (sh.uniform && p0) {
-            for (int j = 0; j < p0->n_in; ++j) {
-                sh.uin[j] = static_cast<uint8_t>(p0->in_stream[j]);
-                if (p0->in_src[j]) sh.src_bits |= 1u << (kUniInSrc + j);
-            }
-            for (int l = 0; l < p0->n_out; ++l) {
-                sh.uout[l] = static_cast<uint8_t>(p0->out_stream[l]);
-                if (p0->out_src[l]) sh.src_bits |= 1u << (kUniOutSrc + l);
-            }
-            sh.streams = sh.en + sh.el;  // the launch's slots after reordering
-        } else {
-            sh.uniform = false;
-        }
-    }
     return sh;
 }
 
@@ -491,24 +457,23 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 enum KernelKind { kKindNarrow, kKindExact, kKindGeneric };
 
 // Every stream a kernel of `kind` will dereference for each used pattern, read from the
-// argument layout it will see (kFlagUniform order or pattern slots), is the stream the
-// pattern names, and is not NULL.  A mismatch is a library bug that would fault the GPU:
-// refuse the launch instead.
+// argument slots it will see (two for the narrow kernels), is the stream the pattern
+// names, and is not NULL.  A mismatch is a library bug (or a NULL arena the op's checks
+// missed) that would fault the GPU: refuse the launch instead.
 static bool stream_layout_ok(const CombineArgs &a, KernelKind kind, const Streams &st, const Pattern *hpats,
                              size_t n_pats, const std::vector<char> *used) {
-    const bool uni = kind != kKindGeneric && (a.flags & kFlagUniform);
     const int slots = kind == kKindNarrow ? kNarrowStreams : kMaxStreams;
     for (size_t q = 0; q < n_pats; ++q) {
         if (used && (q >= used->size() || !(*used)[q])) continue;
         if (!used && (a.flags & kFlagOnePattern) && q > 0) break;
         const Pattern &p = hpats[q];
         for (int i = 0; i < p.n_in; ++i) {
-            const int slot = uni ? i : p.in_stream[i];
-            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[p.in_stream[i]]) return false;
+            const int slot = p.in_stream[i];
+            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[slot]) return false;
         }
         for (int l = 0; l < p.n_out; ++l) {
-            const int slot = uni ? p.n_in + l : p.out_stream[l];
-            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[p.out_stream[l]]) return false;
+            const int slot = p.out_stream[l];
+            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[slot]) return false;
         }
     }
     return true;
@@ -522,23 +487,15 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
     memset(&a, 0, sizeof a);
     a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u) |
               (n_pats == 1 ? kFlagOnePattern : 0u);
-    // Which kernel runs: the stream order of kFlagUniform is read by the exact-shape
-    // kernels only; a shape without one (e.g. 16 inputs) keeps the slot layout its
-    // patterns name.  (sh.streams counts the reordered slots when uniform.)
+    // Which kernel runs: the exact-shape one if the shape has an instantiation, the narrow
+    // two-slot one for 1 x 1 launches over slots 0 and 1, else a capacity kernel.
     const bool exact_k = sh.exact && has_exact(sh.en, sh.el, sh.eacc);
     const KernelKind kind =
         exact_k && sh.en == 1 && sh.el == 1 && sh.streams <= kNarrowStreams &&
                 (sh.eacc == kAccAll || sh.eacc == kAccNone)
             ? kKindNarrow
             : exact_k ? kKindExact : kKindGeneric;
-    if (sh.uniform && kind != kKindGeneric) {
-        // the streams in pattern order: inputs at 0.., outputs at en.. (kFlagUniform)
-        for (int i = 0; i < sh.en; ++i) a.base[i] = st.base[sh.uin[i]];
-        for (int l = 0; l < sh.el; ++l) a.base[sh.en + l] = st.base[sh.uout[l]];
-        a.flags |= kFlagUniform | sh.src_bits;
-    } else {
-        for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
-    }
+    for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
     if (!stream_layout_ok(a, kind, st, hpats, n_pats, used))
         return fail(CEC_EINVAL, "internal: a launch's stream layout does not match its patterns "
                                 "(kind %d, %d x %d); not launched", static_cast<int>(kind), sh.en, sh.el);
