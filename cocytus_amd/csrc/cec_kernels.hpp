@@ -88,9 +88,6 @@ constexpr uint32_t kFlagSysRelease = 1u;
 // dirty lines they would leave in L2 are a visible part of the launch (DESIGN.md §4:
 // the per-GPU shares of strong scaling).
 constexpr uint32_t kFlagWriteThrough = 2u;
-// CombineArgsN::flags: the launch has one pattern; every tile uses it whatever its
-// pattern field says (the ops whose extents' pattern is "ignored", cocytus_ec.h).
-constexpr uint32_t kFlagOnePattern = 4u;
 
 template <int S>
 struct CombineArgsN {
@@ -303,7 +300,7 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         const uint32_t part = static_cast<uint32_t>(g) & ((1u << sh) - 1u);
         const uint32_t lane = (part << (kBlockLog2 - sh)) + threadIdx.x;
         const TileRef tr = load_tile(a, t);
-        const CEC_CONST Pattern *P = as_const(a.patterns) + ((a.flags & kFlagOnePattern) ? 0u : tr.pattern);
+        const CEC_CONST Pattern *P = as_const(a.patterns) + tr.pattern;
         const int n_in = kExact ? NT : P->n_in;
         const int n_out = kExact ? LT : P->n_out;
         if (!kExact && n_out == 0) continue;
@@ -385,7 +382,9 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         }
         compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
         if (wide) {
-            if (a.flags & kFlagWriteThrough) {
+            // (the LDS engine keeps non-temporal stores: the branch alone cost its encode
+            // 1 %, profiles/r03_evidence/lds_engine_ab/)
+            if (!Eng::kStaged && (a.flags & kFlagWriteThrough)) {
 #pragma unroll
                 for (int l = 0; l < LT; ++l)
                     if (l < n_out) st16_wt(out[l], pos, acc[l]);

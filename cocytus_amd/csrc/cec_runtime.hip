@@ -465,7 +465,6 @@ static bool stream_layout_ok(const CombineArgs &a, KernelKind kind, const Stream
     const int slots = kind == kKindNarrow ? kNarrowStreams : kMaxStreams;
     for (size_t q = 0; q < n_pats; ++q) {
         if (used && (q >= used->size() || !(*used)[q])) continue;
-        if (!used && (a.flags & kFlagOnePattern) && q > 0) break;
         const Pattern &p = hpats[q];
         for (int i = 0; i < p.n_in; ++i) {
             const int slot = p.in_stream[i];
@@ -485,8 +484,7 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
                           const std::vector<char> *used, uint32_t flags = 0, bool *released = nullptr) {
     CombineArgs a;
     memset(&a, 0, sizeof a);
-    a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u) |
-              (n_pats == 1 ? kFlagOnePattern : 0u);
+    a.flags = flags | (write_through(n_tiles, sh.nt + sh.lt) ? kFlagWriteThrough : 0u);
     // Which kernel runs: the exact-shape one if the shape has an instantiation, the narrow
     // two-slot one for 1 x 1 launches over slots 0 and 1, else a capacity kernel.
     const bool exact_k = sh.exact && has_exact(sh.en, sh.el, sh.eacc);
@@ -799,9 +797,17 @@ static int encode_common(int k, int m, const int *matrix, const uint8_t *const *
     return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream));
 }
 
+// Ops with one pattern index every tile's pattern field into a one-entry table: it must be 0.
+static int single_pattern_plan(const cec_plan *plan, const char *op) {
+    if (plan->n_ext && plan->max_pattern != 0)
+        return fail(CEC_EINVAL, "%s: extent pattern %u, must be 0 for this op", op, plan->max_pattern);
+    return CEC_OK;
+}
+
 CEC_API int cec_encode(int k, int m, const int *matrix, const uint8_t *const *data,
                        uint8_t *const *parity, const cec_plan *plan, void *stream) {
     if (!plan) return fail(CEC_EINVAL, "cec_encode: plan is NULL");
+    if (int r = single_pattern_plan(plan, "cec_encode")) return r;
     return encode_common(k, m, matrix, data, parity, plan, 0, stream);
 }
 
@@ -925,6 +931,7 @@ CEC_API int cec_residual(int k, int m, const int *matrix, int lid_self, uint32_t
     if (int r = check_code(k, m, matrix)) return r;
     if (lid_self < k || lid_self >= k + m || !arenas || !residual || !plan)
         return fail(CEC_EINVAL, "cec_residual: bad args");
+    if (int r = single_pattern_plan(plan, "cec_residual")) return r;
     int dev;
     if (int r = current_device(&dev)) return r;
     Streams st;
@@ -973,6 +980,7 @@ CEC_API int cec_solve(int k, int m, const int *matrix, uint32_t mask,
     if (int r = check_code(k, m, matrix)) return r;
     if (!mask_ok(k, m, mask) || !residuals || !out || !plan)
         return fail(CEC_EINVAL, "cec_solve: bad args (mask=0x%x)", mask);
+    if (int r = single_pattern_plan(plan, "cec_solve")) return r;
     int dev;
     if (int r = current_device(&dev)) return r;
     int lost[CEC_MAX_K], pars[CEC_MAX_M], inv[CEC_MAX_M * CEC_MAX_M];

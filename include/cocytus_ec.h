@@ -59,8 +59,9 @@ typedef enum cec_status {
  *   cec_diff_update / cec_apply_diffs /
  *   cec_set_diff                       : source data shard lid j (0..k-1)
  *   cec_decode                         : index into the op's mask array
- *   other ops                          : ignored (any value).
- * An index out of range (j >= k, or >= n_masks) makes the op return CEC_EINVAL. */
+ *   other ops (encode, residual, solve): 0.
+ * An index out of range (j >= k, >= n_masks, or not 0) makes the op return
+ * CEC_EINVAL before anything is launched. */
 typedef struct cec_extent {
     uint64_t off;
     uint64_t src_off;

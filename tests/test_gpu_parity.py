@@ -162,29 +162,33 @@ def test_encode_region(gpu, oracle, engine, k, m):
         assert np.array_equal(to_host(pdev[p]), exp[p])
 
 
-def test_extent_pattern_ignored_or_validated(gpu, oracle):
-    """cocytus_ec.h: ops with one pattern ignore the extents' pattern field (any value
-    encodes correctly -- the kernel must not index a table past its one entry); ops that
-    index by it refuse an out-of-range index with CEC_EINVAL before launching."""
+def test_extent_pattern_validated(gpu, oracle):
+    """cocytus_ec.h: every op checks its extents' pattern index before launching (the
+    kernel indexes the op's pattern table with it): single-pattern ops require 0, the
+    others an index below k / n_masks; anything else is CEC_EINVAL and nothing runs."""
     torch, ec = gpu
     k, m, n, B = 3, 2, 4096, 8
     mat = ec.coding_matrix(k, m)
     host = [oracle.splitmix_bytes(70 + j, B * n) for j in range(k)]
     data = [to_dev(torch, h) for h in host]
     parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
-    wild = ec.Plan([(s * n, 0, n, 1000 + 77 * s) for s in range(B)])
-    ec.encode(k, m, mat, data, parity, wild)
+    ok = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
+    ec.encode(k, m, mat, data, parity, ok)
     res = torch.zeros(B * n, dtype=torch.uint8, device="cuda")
     mask = ec.recovery_mask(k, m, k, [0, 1, 1, 1, 1])
-    ec.residual(k, m, mat, k, mask, data + parity, res, wild)
+    wild = ec.Plan([(s * n, 0, n, 1000 + 77 * s) for s in range(B)])
+    for call in (lambda: ec.encode(k, m, mat, data, parity, wild),
+                 lambda: ec.residual(k, m, mat, k, mask, data + parity, res, wild),
+                 lambda: ec.solve(k, m, mat, mask, [None, None, None, res, res], [res, None, None], wild)):
+        with pytest.raises(ec.CecError) as e:
+            call()
+        assert e.value.code == ec.CEC_EINVAL
     torch.cuda.synchronize()
     exp = oracle.encode(mat, k, m, host)
     for p in range(m):
         assert np.array_equal(to_host(parity[p]), exp[p]), p
-    want = exp[0].copy()
-    for j in (1, 2):
-        oracle.region_multiply(host[j], mat[k * k + j], want, 1)
-    assert np.array_equal(to_host(res), want)
+    assert not to_host(res).any()  # nothing launched
+    ok.destroy()
     stage = torch.zeros(B * n, dtype=torch.uint8, device="cuda")
     bad = ec.Plan([(s * n, s * n, n, k if s == B - 1 else s % k) for s in range(B)])
     with pytest.raises(ec.CecError) as e:
