@@ -10,6 +10,7 @@ from __future__ import annotations
 import itertools
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -941,6 +942,29 @@ def test_native_metric_harness(gpu, tmp_path):
     assert r.returncode == 0, r.stderr + r.stdout
     out = json.loads(r.stdout)
     assert out["verified"] is True and out["n_gpus"] == 2
+
+
+def test_bench_two_ranks_one_card_weak_and_strong(gpu):
+    """bench.py --gpus 2 (the driver's multi-GPU entry point) with both ranks on this one
+    card (gloo): one JSON line, n_gpus 2, the weak line verified and the fixed-batch
+    `strong` record (32,768 stripes per rank) verified.  Short steps: this
+    checks the path, not the rates (two ranks share one card)."""
+    import json
+
+    env = {x: v for x, v in os.environ.items()
+           if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["CEC_BENCH_DEVICE"] = "0"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3",
+                        "--warmup", "1", "--also=", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["verified"] is True
+    st = out["strong"]
+    assert st["n_gpus"] == 2 and st["stripes_per_gpu"] == 32768 and st["verified"] is True
+    assert st["value"] > 0
 
 
 def test_graph_capture_replay(gpu, oracle):

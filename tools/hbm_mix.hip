@@ -59,7 +59,8 @@ __global__ __launch_bounds__(256) void k_mix(Ptrs p, uint32_t *sink) {
 //   kind 1: the same without install (4 reads, P0 / P1 written back)
 //   kind 2: RS(3,2) decode with the lost shard rotating per 4 KiB stripe and the leader
 //           every 3 stripes (the bench): reads the 2 surviving data arenas (r0..r2) and
-//           parity r3 / r4, writes out arena w[lost]
+//           parity r3 / r4, writes arena 5 + lost (the bench's arena order; round 2's
+//           probe wrote 6 + lost, one arena further along the slab)
 //   kind 3: RS(4,2) decode, 64 KiB stripes (16 tiles), lost shard rotating per stripe:
 //           reads 3 data (r0..r3) + parity r4 / r5, writes w[lost]
 //   kind 4: kind 2 with a fixed lost shard (D0) and leader (P0)
@@ -84,7 +85,7 @@ __global__ __launch_bounds__(256) void k_shape(Ptrs p, uint8_t *const *all, uint
         for (int j = 0; j < 3; ++j)
             if (j != (int)lost) acc ^= ld(all[j]);
         acc ^= ld(all[3 + par]);
-        st(all[6 + lost], acc);
+        st(all[5 + lost], acc);  // the bench's layout: data 0-2, parity 3-4, rebuilt 5-7
     } else {
         const uint32_t stripe = t >> 4, lost = stripe % 4, par = (stripe / 4) % 2;
         for (int j = 0; j < 4; ++j)
