@@ -18,7 +18,10 @@ Multi-GPU: `bench.py --gpus N` starts N rank processes itself (torch.distributed
 a child, before anything touches the GPU), or runs as one rank of an outer
 `torch.distributed.run --nproc-per-node N bench.py --gpus N`: every rank
 encodes/decodes its own batch (independent stripes, no collective on the data path);
-barrier + synchronize around the timed steps, max over ranks (weak scaling).
+barrier + synchronize around the timed steps, max over ranks (weak scaling: `value`).
+`strong`: the metric's one batch split contiguously over the ranks, whole
+payload / max over ranks; at N = 1 it times the shares a fixed batch gives at N = 2, 4,
+8 on the one GPU instead and reports the implied factor.
 other_workloads also carries the fused per-SET diff-update (the north star's first op)
 and the pinned-host end-to-end path, each with its own roofline / PCIe fraction.
 
