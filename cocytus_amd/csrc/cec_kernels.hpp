@@ -284,14 +284,8 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 // work item g is tile g >> split_shift, part g & (2^split_shift - 1).
 // kSysRel: every wave ends with a system-scope release (kFlagSysRelease launches; a
 // template parameter, so the batched kernels carry no epilogue at all).
-#ifdef CEC_WAVES_PER_EU  // (A/B builds only: a minimum occupancy for the PERM kernels)
-#define CEC_KERNEL_ATTR \
-    __attribute__((amdgpu_waves_per_eu(!Eng::kStaged && kExact && kAcc == kAccNone && NT + LT <= 5 ? CEC_WAVES_PER_EU : 1)))
-#else
-#define CEC_KERNEL_ATTR
-#endif
 template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams, bool kSysRel = false>
-__global__ __launch_bounds__(kBlock) CEC_KERNEL_ATTR void combine_kernel(CombineArgsN<S> a) {
+__global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
     extern __shared__ uint4 cec_lds_rows[];  // LDS engine: the pattern's product rows
     const uint8_t *lds = reinterpret_cast<const uint8_t *>(cec_lds_rows);
     const uint32_t sh = a.split_shift;
