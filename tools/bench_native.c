@@ -14,6 +14,8 @@
  * own batch (no collective); a barrier before and after the timed steps; the time is the
  * max over threads and the value all threads' payload over it.  CEC_NATIVE_DEVICE=d puts
  * every thread on device d (a one-card rehearsal of the threaded path).
+ * CEC_NATIVE_STRIPES=b runs b stripes per GPU instead of 65,536: the per-GPU share of
+ * the strong-scaling split (8,192 at 8 GPUs), timed with no Python in the loop.
  *   usage: bench_native [S [W [G]]]        make -C tools   (needs cocytus_amd/libcocytus_ec.so)
  */
 #include <cocytus_ec.h>
@@ -37,7 +39,8 @@
     } while (0)
 
 enum { K = 3, M = 2, NMASK = K * M };
-static const size_t n = 4096, B = 65536;
+static const size_t n = 4096;
+static size_t B = 65536; /* stripes per GPU; CEC_NATIVE_STRIPES: one GPU's share of a fixed batch */
 
 typedef struct {
     int device, S, W, rc;
@@ -169,6 +172,12 @@ int main(int argc, char **argv) {
     const int S = argc > 1 ? atoi(argv[1]) : 20, W = argc > 2 ? atoi(argv[2]) : 3;
     int G = argc > 3 ? atoi(argv[3]) : 1, ndev = 0;
     const char *pin = getenv("CEC_NATIVE_DEVICE");
+    const char *stripes = getenv("CEC_NATIVE_STRIPES");
+    if (stripes && *stripes) B = (size_t)strtoull(stripes, NULL, 0);
+    if (B < NMASK || B > 65536) {
+        fprintf(stderr, "CEC_NATIVE_STRIPES = %zu outside [%d, 65536]\n", B, NMASK);
+        return 1;
+    }
     if (cec_device_count(&ndev) != CEC_OK || ndev < 1 || cec_device_check() != CEC_OK) {
         fprintf(stderr, "no usable gfx950 device: %s\n", cec_last_error());
         return 1;
@@ -205,10 +214,10 @@ int main(int argc, char **argv) {
            "\"harness\": \"tools/bench_native.c (C-ABI only, no Python / torch; one thread per GPU)\", "
            "\"value\": %.2f, \"unit\": \"GiB/s\", \"n_gpus\": %d, \"devices\": \"%s\", \"steps\": %d, "
            "\"warmup\": %d, \"ms_per_step\": %.4f, \"encode_ms\": %.4f, \"encode_frac\": %.4f, "
-           "\"decode_ms\": %.4f, \"decode_frac\": %.4f, \"verified\": %s}\n",
+           "\"decode_ms\": %.4f, \"decode_frac\": %.4f, \"stripes_per_gpu\": %zu, \"verified\": %s}\n",
            el > 0 ? payload / el / (double)(1u << 30) : 0.0, G, pin ? "one card (CEC_NATIVE_DEVICE)" : "0..G-1",
            S, W, el * 1e3 / S, enc, (double)(K + M) * L / (enc * 1e-3) / 8e12, dec,
-           (double)(K + 1) * L / (dec * 1e-3) / 8e12, (bad || rc) ? "false" : "true");
+           (double)(K + 1) * L / (dec * 1e-3) / 8e12, B, (bad || rc) ? "false" : "true");
     pthread_barrier_destroy(&bar);
     free(args);
     free(tid);

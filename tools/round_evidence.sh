@@ -29,6 +29,9 @@ timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
 timeout -k 10 200 tools/pool_bench.bin     > "$OUT/pool_bench.jsonl" 2>&1
 timeout -k 10 200 tools/launch_latency.bin > "$OUT/launch_latency.txt" 2>&1
 timeout -k 10 200 tools/bench_native.bin 20 3 > "$OUT/bench_native.jsonl" 2>&1
+for b in 32768 16384 8192; do  # the strong-scaling shares with no Python in the loop
+  CEC_NATIVE_STRIPES=$b timeout -k 10 200 tools/bench_native.bin 20 3 >> "$OUT/bench_native_shares.jsonl" 2>&1
+done
 CEC_NATIVE_DEVICE=0 timeout -k 10 200 tools/bench_native.bin 20 3 2 > "$OUT/bench_native_2threads_one_card.jsonl" 2>&1
 CEC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 > "$OUT/bench_gloo2_one_card.jsonl" 2> "$OUT/bench_gloo2.err"
 # the driver's N: 8 ranks on one card (gloo), the weak line and the fixed-batch split
