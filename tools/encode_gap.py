@@ -4,7 +4,9 @@ One process, the bench's arenas, interleaved rounds (not product):
   plan      cec_encode over the 65,536-extent plan (the bench's kernel)
   region    cec_encode_region: the same bytes as one implicit range (no tile list)
   xor       cec_encode_region with both parity rows all ones (no GF multiply)
-  plan_xor  the plan with the all-ones matrix"""
+  plan_xor  the plan with the all-ones matrix
+ENCODE_GAP_STRIPES=b: b stripes instead of 65,536 (the strong-scaling shares: is the
+small launch's fixed cost in the tile list, the GF multiply or neither?)"""
 import os
 import sys
 
@@ -17,7 +19,8 @@ torch.cuda.set_device(0)
 torch.empty(1, device="cuda")
 from cocytus_amd import ec  # noqa: E402
 
-k, m, n, B = 3, 2, 4096, 65536
+k, m, n = 3, 2, 4096
+B = int(os.environ.get("ENCODE_GAP_STRIPES", "65536"))
 L = n * B
 mat = ec.coding_matrix(k, m)
 ones = mat[:k * k] + [1] * (m * k)
@@ -44,6 +47,7 @@ for rnd in range(8):
             fn()
         b.record(s)
         res[name].append(a.elapsed_ms(b) / 10)
+print(f"stripes {B}")
 for name, v in res.items():
     v.sort()
     print(f"{name:9s} median {v[len(v) // 2] * 1e3:7.1f} us  {5 * L / (v[len(v) // 2] * 1e-3) / 1e9:6.0f} GB/s  "
