@@ -49,10 +49,22 @@ __device__ inline void store16(uint8_t *base, uint32_t bytes, uint32_t off, u32x
     }
 }
 
-template <int W, int AUX>
+// A cold path of byte gathers the launch never takes (a.bytes is never 0 here): it only
+// makes the kernel's code as large as the library's (kBig), to see whether code size --
+// instruction-cache warm-up at the start of a launch -- is a per-launch cost.
+template <int W, int AUX, bool kBig = false>
 __global__ __launch_bounds__(64) void k_stream(Args a) {
     const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
     u32x4 acc = {0, 0, 0, 0};
+    if constexpr (kBig) {
+        if (a.bytes == 0) {
+            uint32_t v[160];
+#pragma unroll
+            for (int b = 0; b < 160; ++b) v[b] = *(const GL uint8_t *)((uintptr_t)a.r[b % 3] + off + (b * 7919u) % 4096u);
+#pragma unroll
+            for (int b = 0; b < 160; ++b) *(GL uint8_t *)((uintptr_t)a.w[b & 1] + off + (b * 104729u) % 4096u) = (uint8_t)(v[b] ^ v[(b + 5) % 160]);
+        }
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) acc ^= __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)a.r[i] + off));
 #pragma unroll
@@ -72,7 +84,7 @@ __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
     }
 }
 
-template <int AUX>
+template <int AUX, bool kBig = false>
 static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps, double fit[2][2]) {
     const uint32_t sizes[] = {8192, 16384, 65536};
     for (uint32_t stripes : sizes) {
@@ -83,15 +95,15 @@ static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps
         std::vector<hipEvent_t> ev(2 * steps + 1);
         for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         for (int w = 0; w < 3; ++w) {
-            k_stream<2, AUX><<<grid, 64>>>(enc);
-            k_stream<1, AUX><<<grid, 64>>>(dec);
+            k_stream<2, AUX, kBig><<<grid, 64>>>(enc);
+            k_stream<1, AUX, kBig><<<grid, 64>>>(dec);
         }
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(ev[0], 0));
         for (int s = 0; s < steps; ++s) {
-            k_stream<2, AUX><<<grid, 64>>>(enc);
+            k_stream<2, AUX, kBig><<<grid, 64>>>(enc);
             CK(hipEventRecord(ev[2 * s + 1], 0));
-            k_stream<1, AUX><<<grid, 64>>>(dec);
+            k_stream<1, AUX, kBig><<<grid, 64>>>(dec);
             CK(hipEventRecord(ev[2 * s + 2], 0));
         }
         CK(hipDeviceSynchronize());
@@ -141,6 +153,8 @@ int main(int argc, char **argv) {
         run<0>("plain", ar, stride, steps, fit);
         run<16>("sc1", ar, stride, steps, fit);
         run<18>("sc1nt", ar, stride, steps, fit);
+        run<16, true>("sc1_bigcode", ar, stride, steps, fit);
+        run<-1, true>("nt_bigcode", ar, stride, steps, fit);
     }
     CK(hipFree(slab));
     return 0;
