@@ -1,0 +1,138 @@
+#!/bin/bash
+# Round-3 gpurun calls, one case per call: `gpurun -- bash tools/r03_calls.sh <letter>`.
+# Each GPU step runs under its own timeout; a step that faults, aborts or times out
+# ends the call. The letter names the gpurun_out/r03<letter>/ directory the call wrote,
+# whose kept files are under profiles/r03_evidence/.
+call=$1
+mkdir -p gpurun_out/r03$call
+run() { name=$1; shift; timeout -k 10 "$@" > gpurun_out/r03$call/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; if [ $rc -gt 1 ]; then exit $rc; fi; }
+case "$call" in
+b)
+  # round-3 GPU step list (one call): full GPU suite, the stale-tile precondition probe and
+  # negative control, the small-batch fixed-cost probe, the diff-update early-install A/B
+  run pytest 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
+  run xcdvis 120 tools/xcd_visibility_probe.bin 64 200
+  run prefix_neg 300 env CEC_LIB_PATH=tools/prefix_build/libcocytus_ec.so python -u -m pytest tests/test_gpu_parity.py -k visible_from_every_xcd -q --timeout 120 --timeout-method thread
+  run smallbatch 120 tools/small_batch_probe.bin 20
+  for i in 1 2 3; do
+    run du_new_$i 200 python -u bench.py --also=rs32_diff_update --no-strong --no-cpu-baseline
+    run du_old_$i 200 env CEC_LIB_PATH=tools/ab_du/libcocytus_ec.so python -u bench.py --also=rs32_diff_update --no-strong --no-cpu-baseline
+  done
+  ;;
+c)
+  # round-3 GPU steps: store-policy A/B on the strong-scaling shares, GPU suite under
+  # forced write-through and under the default policy, box record for the stale-tile probe
+  run xcdvis 120 tools/xcd_visibility_probe.bin 64 200
+  run pytest_wt 700 env CEC_STORE_POLICY=wt python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
+  for i in 1 2 3; do
+    for p in nt wt auto; do
+      run bench_${p}_$i 200 env CEC_STORE_POLICY=$p python -u bench.py --also= --no-cpu-baseline
+    done
+  done
+  run pytest_auto 700 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
+  ;;
+e)
+  # round-3 GPU steps: uniform-stream launches (kFlagUniform) -- GPU suite, then A/B against
+  # the previous build (tools/ab_prev) on the metric and its strong-scaling shares, and --ops
+  run xcdvis 120 tools/xcd_visibility_probe.bin 64 200
+  run pytest 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+  for i in 1 2 3; do
+    run bench_new_$i 200 python -u bench.py --also= --no-cpu-baseline
+    run bench_prev_$i 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u bench.py --also= --no-cpu-baseline
+  done
+  run ops_new 200 python -u bench.py --ops
+  run ops_prev 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u bench.py --ops
+  ;;
+f)
+  # round-3 evidence on the final kernels: GPU suite, then every DESIGN §5 number (no profiles)
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r03f/pytest.log 2>&1 && \
+  EVID_NO_PROF=1 bash tools/round_evidence.sh r03
+  ;;
+g)
+  # round-3 GPU steps: LDS-engine A/B -- this build (no write-through branch in the staged
+  # kernels) vs the branch (tools/ab_lds_wt) vs the build before the store policy (tools/ab_lds_pre)
+  B="python -u bench.py --engine lds --also= --no-cpu-baseline --no-strong"
+  for i in 1 2 3; do
+    run lds_new_$i 200 $B
+    run lds_wt_$i 200 env CEC_LIB_PATH=tools/ab_lds_wt/libcocytus_ec.so $B
+    run lds_pre_$i 200 env CEC_LIB_PATH=tools/ab_lds_pre/libcocytus_ec.so $B
+  done
+  run pytest_lds 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "lds or golden or fuzz"
+  ;;
+h)
+  # round-3 evidence on the final kernels (after the LDS fix): GPU suite, then every DESIGN §5 number (no profiles)
+  timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r03h/pytest.log 2>&1 && \
+  EVID_NO_PROF=1 bash tools/round_evidence.sh r03
+  ;;
+i)
+  # round-3 rocprofv3 evidence on the final kernels: kernel-trace + FETCH_SIZE / WRITE_SIZE
+  # passes per workload, default (PERM) engine, then the LDS engine for the metric and the
+  # diff-update
+  bash tools/profile_round.sh r03 || exit $?
+  PROF_ENGINE=lds PROF_WORKLOADS="rs32_4k rs32_diff_update" bash tools/profile_round.sh r03_lds || exit $?
+  ;;
+j)
+  # round-3 sanitizer runs on the final host code (pool tables, launch checks, cache changes)
+  timeout -k 10 600 bash tools/asan.sh run > gpurun_out/r03j/asan.txt 2>&1 && \
+  timeout -k 10 600 bash tools/tsan.sh run > gpurun_out/r03j/tsan.txt 2>&1
+  ;;
+k)
+  # round-3: the two-rank bench test, and the decode shape ceiling in the bench's arena order
+  # beside the library's decode in the same call
+  run pytest2 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "two_ranks or edge_cases or extent_pattern"
+  run hbm_mix 200 tools/hbm_mix.bin arena random 64
+  run decode_probe 200 python -u tools/decode_probe.py
+  run hbm_mix_b 200 tools/hbm_mix.bin arena random 64
+  ;;
+l)
+  # round-3: workgroups per tile (CEC_SPLIT_SHIFT) at the strong-scaling shares
+  for i in 1 2; do
+    for sh in 2 1 0; do
+      run split${sh}_$i 200 env CEC_SPLIT_SHIFT=$sh python -u bench.py --also= --no-cpu-baseline
+    done
+  done
+  ;;
+m)
+  # round-3: occupancy floor of 8 waves per SIMD for the small exact PERM kernels
+  # (tools/ab_occ, -DCEC_WAVES_PER_EU=8: encode 3x2 68 -> 64 VGPRs) vs this build
+  for i in 1 2 3; do
+    run cur_$i 200 python -u bench.py --also= --no-cpu-baseline
+    run occ_$i 200 env CEC_LIB_PATH=tools/ab_occ/libcocytus_ec.so python -u bench.py --also= --no-cpu-baseline
+  done
+  ;;
+n)
+  # round-3: the metric's step through the C-ABI alone at the strong-scaling shares
+  for i in 1 2; do
+    for b in 65536 32768 16384 8192; do
+      CEC_NATIVE_STRIPES=$b timeout -k 10 200 tools/bench_native.bin 20 3 >> gpurun_out/r03n/native_shares.jsonl 2>&1 || exit $?
+    done
+  done
+  ;;
+o)
+  # round-3: where a small encode launch's fixed cost goes (tile list / GF multiply / neither)
+  for b in 8192 65536 8192; do
+    ENCODE_GAP_STRIPES=$b timeout -k 10 200 python -u tools/encode_gap.py >> gpurun_out/r03o/encode_gap.txt 2>&1 || exit $?
+  done
+  timeout -k 10 120 tools/small_batch_probe.bin 20 > gpurun_out/r03o/small_batch_probe.jsonl 2>&1
+  ;;
+p)
+  # round-3: LDS engine, workgroups per tile (its rotating decode stages product rows per
+  # workgroup: 768 B per 1 KiB quarter-tile with s = 2)
+  for i in 1 2; do
+    for sh in 2 1 0; do
+      run lds_s${sh}_$i 200 env CEC_SPLIT_SHIFT=$sh python -u bench.py --engine lds --also= --no-cpu-baseline --no-strong
+    done
+  done
+  ;;
+q)
+  # round-3 final check on the final tree, as the driver runs it: GPU suite, smoke, default bench
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03q/pytest.log 2>&1 && \
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03q/smoke.log 2>&1 && \
+  timeout -k 10 600 python -u bench.py > gpurun_out/r03q/bench_default.jsonl 2> gpurun_out/r03q/bench_default.err
+  ;;
+r)
+  # round-3: does a kernel's code size cost a small launch (instruction-cache warm-up)?
+  timeout -k 10 200 tools/small_batch_probe.bin 20 > gpurun_out/r03r/small_batch_probe_v3.jsonl 2>&1
+  ;;
+*) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
+esac
