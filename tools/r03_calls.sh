@@ -134,5 +134,10 @@ r)
   # round-3: does a kernel's code size cost a small launch (instruction-cache warm-up)?
   timeout -k 10 200 tools/small_batch_probe.bin 20 > gpurun_out/r03r/small_batch_probe_v3.jsonl 2>&1
   ;;
+s)
+  # round-3: the bare stream with 64-bit vector addresses (what the code-size variant's
+  # hot path compiled to) against the scalar-base form the library uses
+  timeout -k 10 200 tools/small_batch_probe.bin 20 > gpurun_out/r03s/small_batch_probe_vaddr2.jsonl 2>&1
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac

@@ -49,14 +49,16 @@ __device__ inline void store16(uint8_t *base, uint32_t bytes, uint32_t off, u32x
     }
 }
 
-// A cold path of byte gathers the launch never takes (a.bytes is never 0 here): it only
-// makes the kernel's code as large as the library's (kBig), to see whether code size --
-// instruction-cache warm-up at the start of a launch -- is a per-launch cost.
-template <int W, int AUX, bool kBig = false>
+// kMode 1: a cold path of byte copies the launch never takes; it only makes the kernel's
+// code as large as the library's, to see whether code size (instruction-cache warm-up at
+// the start of a launch) is a per-launch cost.  kMode 2: no cold path, but every load
+// and nt store through a 64-bit vector address instead of a scalar base + 32-bit vector
+// offset (what kMode 1's hot path compiled to), to separate the addressing form.
+template <int W, int AUX, int kMode = 0>
 __global__ __launch_bounds__(64) void k_stream(Args a) {
     const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
     u32x4 acc = {0, 0, 0, 0};
-    if constexpr (kBig) {
+    if constexpr (kMode == 1) {
         if (blockIdx.x == 0xffffffffu) {  // never: the id is already in an SGPR, no wait
             // byte copies one at a time (the empty asm keeps them from being batched, so
             // the register count stays the fast variant's; only the code grows)
@@ -69,12 +71,22 @@ __global__ __launch_bounds__(64) void k_stream(Args a) {
         }
     }
 #pragma unroll
-    for (int i = 0; i < 3; ++i) acc ^= __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)a.r[i] + off));
+    for (int i = 0; i < 3; ++i) {
+        const GL u32x4 *p = (const GL u32x4 *)((uintptr_t)a.r[i] + off);
+        if constexpr (kMode == 2) asm volatile("" : "+v"(p));
+        acc ^= __builtin_nontemporal_load(p);
+    }
 #pragma unroll
     for (int j = 0; j < W; ++j) {
         u32x4 v = acc;
         v.x ^= j;
-        store16<AUX>(a.w[j], a.bytes, off, v);
+        if constexpr (kMode == 2 && AUX < 0) {
+            GL u32x4 *q = (GL u32x4 *)((uintptr_t)a.w[j] + off);
+            asm volatile("" : "+v"(q));
+            __builtin_nontemporal_store(v, q);
+        } else {
+            store16<AUX>(a.w[j], a.bytes, off, v);
+        }
     }
 }
 
@@ -87,7 +99,7 @@ __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
     }
 }
 
-template <int AUX, bool kBig = false>
+template <int AUX, int kMode = 0>
 static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps, double fit[2][2]) {
     const uint32_t sizes[] = {8192, 16384, 65536};
     for (uint32_t stripes : sizes) {
@@ -98,15 +110,15 @@ static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps
         std::vector<hipEvent_t> ev(2 * steps + 1);
         for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         for (int w = 0; w < 3; ++w) {
-            k_stream<2, AUX, kBig><<<grid, 64>>>(enc);
-            k_stream<1, AUX, kBig><<<grid, 64>>>(dec);
+            k_stream<2, AUX, kMode><<<grid, 64>>>(enc);
+            k_stream<1, AUX, kMode><<<grid, 64>>>(dec);
         }
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(ev[0], 0));
         for (int s = 0; s < steps; ++s) {
-            k_stream<2, AUX, kBig><<<grid, 64>>>(enc);
+            k_stream<2, AUX, kMode><<<grid, 64>>>(enc);
             CK(hipEventRecord(ev[2 * s + 1], 0));
-            k_stream<1, AUX, kBig><<<grid, 64>>>(dec);
+            k_stream<1, AUX, kMode><<<grid, 64>>>(dec);
             CK(hipEventRecord(ev[2 * s + 2], 0));
         }
         CK(hipDeviceSynchronize());
@@ -156,8 +168,10 @@ int main(int argc, char **argv) {
         run<0>("plain", ar, stride, steps, fit);
         run<16>("sc1", ar, stride, steps, fit);
         run<18>("sc1nt", ar, stride, steps, fit);
-        run<16, true>("sc1_bigcode", ar, stride, steps, fit);
-        run<-1, true>("nt_bigcode", ar, stride, steps, fit);
+        run<16, 1>("sc1_bigcode", ar, stride, steps, fit);
+        run<-1, 1>("nt_bigcode", ar, stride, steps, fit);
+        run<16, 2>("sc1_vaddr", ar, stride, steps, fit);
+        run<-1, 2>("nt_vaddr", ar, stride, steps, fit);
     }
     CK(hipFree(slab));
     return 0;
