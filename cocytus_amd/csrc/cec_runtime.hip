@@ -451,8 +451,8 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 // One launch over n_tiles (> 0) tiles of a plan or an implicit region, with the tables
 // (n_pats patterns, then the LDS engine's rows) already on the device.  The caller
 // checks hipGetLastError.
-// *released: whether kFlagSysRelease (if set) was honoured (only the narrow 1 x 1 launches
-// carry the release epilogue).  hpats / used: the host copies of the launch's patterns and
+// *released: whether every wave of the launch ends with a system-scope release
+// (kFlagSysRelease asked for, and honoured: only the narrow 1 x 1 launches carry it).  hpats / used: the host copies of the launch's patterns and
 // which of them its tiles name (NULL: all), for the stream check below.
 enum KernelKind { kKindNarrow, kKindExact, kKindGeneric };
 
@@ -528,7 +528,7 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
     }
     if (!ok) return fail(CEC_EINVAL, "internal: no %s kernel for %d x %d", kind == kKindNarrow ? "narrow" : "exact",
                          sh.en, sh.el);
-    if (released) *released = kind == kKindNarrow || (flags & kFlagSysRelease) == 0;
+    if (released) *released = kind == kKindNarrow && (flags & kFlagSysRelease) != 0;
     return CEC_OK;
 }
 
@@ -1102,9 +1102,12 @@ thread_local SignalCtx t_signal;
 // (tools/launch_latency.hip, archive/profiles/r01_launch_latency.txt).  After 200 us (a large
 // op, or a kernel that faulted and never signals) it falls back to
 // hipStreamSynchronize, which also reports errors.
-// `host_results`: the work wrote host memory that the caller reads on return, and its
-// kernels did not end with their own system-scope release (kFlagSysRelease).
-static int stream_wait(hipStream_t s, bool host_results) {
+// `host_results`: the work wrote host-visible memory that the caller reads on return;
+// `waves_released`: every wave that wrote it ended with its own system-scope release
+// (kFlagSysRelease).  The completion is recorded for cec_last_sync.
+thread_local cec_sync_record t_last_sync = {0, 0, 0, 0};
+
+static int stream_wait(hipStream_t s, bool host_results, bool waves_released = false) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev));
     SignalCtx &c = t_signal;
@@ -1122,6 +1125,11 @@ static int stream_wait(hipStream_t s, bool host_results) {
         c.device = dev;
     }
     const uint32_t v = ++c.seq;
+    const bool fence = host_results && !waves_released;
+    t_last_sync.seq += 1;
+    t_last_sync.host_results = host_results;
+    t_last_sync.waves_released = host_results && waves_released;
+    t_last_sync.fenced = fence;
     // The op's stores into host memory may still sit in the L2 of the XCDs its
     // workgroups ran on, and the signal kernel's own fence writes back only its XCD's
     // (a 4098-byte drop-in call read back its second tile stale on some boxes).  Either
@@ -1131,7 +1139,7 @@ static int stream_wait(hipStream_t s, bool host_results) {
     // call on one box, archive/profiles/r02_evidence_s3/fence_cost_ab.jsonl).  (Spinning on
     // hipEventQuery of that event instead of the signal kernel's flag measured the same
     // per call: archive/profiles/r02_evidence_s3/wait_mode_ab.jsonl.)
-    if (host_results) HIP_TRY(hipEventRecord(c.fence, s));
+    if (fence) HIP_TRY(hipEventRecord(c.fence, s));
     hipLaunchKernelGGL(cec_signal_kernel, dim3(1), dim3(1), 0, s, c.flag_dev, v);
     HIP_TRY(hipGetLastError());
     const auto t0 = std::chrono::steady_clock::now();
@@ -1142,6 +1150,12 @@ static int stream_wait(hipStream_t s, bool host_results) {
             break;
     }
     HIP_TRY(hipStreamSynchronize(s));
+    return CEC_OK;
+}
+
+CEC_API int cec_last_sync(cec_sync_record *out) {
+    if (!out) return fail(CEC_EINVAL, "cec_last_sync: out is NULL");
+    *out = t_last_sync;
     return CEC_OK;
 }
 
@@ -1394,9 +1408,9 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
     bool hs = false, hd = false;
     void *vs = device_view(region, &hs), *vd = device_view(dst, &hd);
     if (vs && vd) {  // device-resident (or pinned/mapped): run in place
-        bool rel = true;  // (a pinned destination: the kernel's waves release it themselves)
+        bool rel = false;  // (a host-visible destination: the kernel's waves release it themselves)
         DROPIN_CHECK(region_launch(dev, vs, multby, n, vd, mode_add, c.stream, true, hd ? kFlagSysRelease : 0, &rel));
-        DROPIN_CHECK(stream_wait(c.stream, !rel));
+        DROPIN_CHECK(stream_wait(c.stream, hd, rel));
         return;
     }
     const size_t n16 = (n + 15) & ~size_t(15);  // the kernel's extent in the staging
@@ -1417,7 +1431,7 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         // results are not copied back)
         bool rel = false;
         DROPIN_CHECK(region_launch(dev, ds, multby, n16, dd, mode_add, c.stream, true, kFlagSysRelease, &rel));
-        DROPIN_CHECK(stream_wait(c.stream, !rel));  // (spinning on hipStreamQuery instead: no gain)
+        DROPIN_CHECK(stream_wait(c.stream, true, rel));  // (spinning on hipStreamQuery instead: no gain)
         memcpy(dst, zd, n);
         return;
     }
@@ -1441,4 +1455,9 @@ CEC_API void galois_w08_region_multiply(char *region, int multby, int nbytes, ch
         DROPIN_HIP(hipMemcpyAsync(dst + o, c.ddst, len, hipMemcpyDefault, c.stream));
         DROPIN_HIP(hipStreamSynchronize(c.stream));
     }
+    // (the result came back by DMA, complete and visible when the stream synchronised)
+    t_last_sync.seq += 1;
+    t_last_sync.host_results = !vd || hd;
+    t_last_sync.waves_released = 0;
+    t_last_sync.fenced = 1;
 }

@@ -79,6 +79,13 @@ class CacheInfo(ctypes.Structure):
         "pattern_entry_limit", "device_cached_bytes", "pinned_cached_bytes")]
 
 
+class SyncRecord(ctypes.Structure):
+    """cec_sync_record (cocytus_ec.h): how the thread's last synchronous call made its
+    results visible to the host."""
+    _fields_ = [("seq", ctypes.c_uint64), ("host_results", ctypes.c_int),
+                ("waves_released", ctypes.c_int), ("fenced", ctypes.c_int)]
+
+
 _vp = ctypes.c_void_p
 _i = ctypes.c_int
 _u32 = ctypes.c_uint32
@@ -140,6 +147,7 @@ _SIGS = {
     "cec_recovery_pool_end": ([_vp, _i], _i),
     "cec_recovery_pool_active": ([_vp], _i),
     "cec_cache_get_info": ([ctypes.POINTER(CacheInfo)], _i),
+    "cec_last_sync": ([ctypes.POINTER(SyncRecord)], _i),
     "cec_cache_set_pattern_limit": ([_i], _i),
     "cec_cache_trim": ([], _i),
     "cec_event_create": ([ctypes.POINTER(_vp)], _i),
@@ -271,6 +279,13 @@ def cache_info() -> dict:
     ci = CacheInfo()
     _check(lib().cec_cache_get_info(ctypes.byref(ci)))
     return {n: int(getattr(ci, n)) for n, _ in CacheInfo._fields_}
+
+
+def last_sync() -> dict:
+    """cec_last_sync: the calling thread's last synchronous completion, as a dict."""
+    r = SyncRecord()
+    _check(lib().cec_last_sync(ctypes.byref(r)))
+    return {n: int(getattr(r, n)) for n, _ in SyncRecord._fields_}
 
 
 def cache_set_pattern_limit(entries: int) -> None:

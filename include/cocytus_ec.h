@@ -341,6 +341,22 @@ int cec_cache_set_pattern_limit(int entries);      /* default 4096 (CEC_PATTERN_
  * graph (synchronises the current device first). */
 int cec_cache_trim(void);
 
+/* ---- completion record (diagnostics) ----
+ * How the calling thread's last synchronous completion (the drop-in
+ * galois_w08_region_multiply, cec_recovery_fold_update / _solve / _finish, the pool's
+ * flush_solve / solve) made its results visible to the host on return.  A result in
+ * host-visible memory (pinned, mapped or managed) may still sit in the L2 of the XCD
+ * that wrote it; it is visible only if every writing wave ended with a system-scope
+ * release or a system-scope fence ran behind the op.  Tests assert the protocol with it
+ * on any box, whether or not the box's host mappings expose a missing release. */
+typedef struct cec_sync_record {
+    uint64_t seq;           /* synchronous completions on this thread so far */
+    int host_results;       /* the op wrote host-visible memory */
+    int waves_released;     /* every writing wave ended with a system-scope release */
+    int fenced;             /* a system-scope fence ran behind the op (fence event or stream sync) */
+} cec_sync_record;
+int cec_last_sync(cec_sync_record *out);
+
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ----
  * Events are for timing: recorded without the system-scope fence, so waiting on one
  * does not make results written into host memory visible.  Use cec_stream_synchronize

@@ -179,3 +179,58 @@ def test_headers_are_c99_and_cxx(tmp_path):
                     "-o", str(tmp_path / "h.o")], check=True)
     subprocess.run(["g++", "-std=c++11", "-Wall", "-Werror", "-I", inc, "-x", "c++", "-c", str(src),
                     "-o", str(tmp_path / "hpp.o")], check=True)
+
+
+LLVM_OBJDUMP = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="llvm-objdump not in this image")
+def test_release_epilogue_in_gfx950_code(lib, tmp_path):
+    """Round 2's stale-tile defect, checked in the shipped machine code on any host: every
+    kSysRel instantiation of combine_kernel (the drop-in's host-visible launches) ends each
+    wave with the system-scope L2 writeback `buffer_wbl2 sc0 sc1` followed by
+    `s_waitcnt vmcnt(0)` before `s_endpgm`, with nothing in between; no other combine
+    kernel writes back L2 (the batched kernels pay nothing).  The GPU tests assert the
+    host side (which launches get it, cec_last_sync)."""
+    import shutil
+
+    so = tmp_path / "lib.so"
+    shutil.copy(os.path.realpath(lib.LIB_PATH), so)
+    subprocess.run([LLVM_OBJDUMP, "--offloading", str(so)], cwd=tmp_path, check=True,
+                   capture_output=True)
+    cos = [p for p in tmp_path.iterdir() if p.name.endswith("gfx950")]
+    assert len(cos) == 1, sorted(p.name for p in tmp_path.iterdir())
+    dis = subprocess.run([LLVM_OBJDUMP, "-d", str(cos[0])], check=True, capture_output=True,
+                         text=True).stdout
+    funcs: dict[str, list[str]] = {}
+    cur = None
+    for line in dis.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
+        if m:
+            cur = m.group(1)
+            funcs[cur] = []
+        elif cur and line.startswith("\t") and not line.startswith("\t\t"):
+            funcs[cur].append(line.split("//")[0].strip())
+    combine = {f: ins for f, ins in funcs.items() if "combine_kernel" in f}
+    assert len(combine) > 50, len(combine)
+    released = {}
+    for f, ins in combine.items():
+        m = re.search(r"Lb([01])EEEvNS_12CombineArgsN", f)
+        assert m, f
+        released[f] = m.group(1) == "1"
+    sysrel = [f for f, r in released.items() if r]
+    # the narrow 1 x 1 kernels: both engines x (write, XOR-accumulate)
+    assert len(sysrel) == 4 and {("Perm" in f, "ELi1ELb1ELi2" in f) for f in sysrel} == {
+        (p, a) for p in (True, False) for a in (True, False)}, sysrel
+    for f, ins in combine.items():
+        wb = [i for i in ins if i.startswith("buffer_wbl2")]
+        ends = [k for k, i in enumerate(ins) if i == "s_endpgm"]
+        assert ends, f
+        if not released[f]:
+            assert not wb, (f, wb)
+            continue
+        for e in ends:
+            k = e - 1
+            while ins[k] == "s_waitcnt vmcnt(0)":
+                k -= 1
+            assert k < e - 1 and ins[k] == "buffer_wbl2 sc0 sc1", (f, ins[max(0, e - 6):e + 1])

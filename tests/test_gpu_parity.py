@@ -654,6 +654,10 @@ def test_dropin_host_buffers(gpu, oracle):
                 ec.galois_w08_region_multiply(buf[so:], c, n, dst[do:], 1)
                 bad = np.flatnonzero(dst != exp)
                 assert bad.size == 0, (n, so, do, c, bad.size, bad[:8].tolist(), bad[-8:].tolist())
+                if c:  # zero-copy: the waves release the mapped staging; staged: DMA + sync
+                    rec = ec.last_sync()
+                    want = (1, 1, 0) if n <= 256 << 10 else (1, 0, 1)
+                    assert (rec["host_results"], rec["waves_released"], rec["fenced"]) == want, (n, rec)
 
 
 def test_dropin_mixed_buffers(gpu, oracle):
@@ -683,6 +687,8 @@ def test_dropin_mixed_buffers(gpu, oracle):
         pa = torch.from_numpy(a.copy()).pin_memory()
         pb = torch.from_numpy(b.copy()).pin_memory()
         ec.galois_w08_region_multiply(pa[5:], 0x53, n, pb[3:], 1)
+        rec = ec.last_sync()
+        assert (rec["host_results"], rec["waves_released"], rec["fenced"]) == (1, 1, 0), (n, rec)
         assert np.array_equal(pb.numpy(), exp), ("pinned -> pinned", n)
 
 
@@ -739,6 +745,11 @@ def test_dropin_host_result_visible_from_every_xcd(gpu, oracle, kind):
             ec.galois_w08_region_multiply(dsrc, c, n, p.value, 1)
             bad = np.flatnonzero(dst != exp)  # read on return: no synchronize
             assert bad.size == 0, (kind, rep, c, bad.size, sorted(set((bad // 4096).tolist()))[:16])
+            # the protocol itself, on any box (round 2's defect was a missing release that
+            # only some boxes' host mappings exposed): every writing wave released its
+            # XCD's L2, and no fence event was spent on top of it
+            rec = ec.last_sync()
+            assert (rec["host_results"], rec["waves_released"], rec["fenced"]) == (1, 1, 0), (kind, rec)
     finally:
         torch.cuda.synchronize()
         (L.hipFree if kind == "managed" else L.hipHostFree)(p)
@@ -752,6 +763,8 @@ def test_dropin_device_buffers(gpu, oracle):
     oracle.region_multiply(a, 0x8E, exp, 1)
     da, db = to_dev(torch, a), to_dev(torch, b)
     ec.galois_w08_region_multiply(da, 0x8E, 10000, db, 1)
+    rec = ec.last_sync()  # a device result: neither release nor fence is paid for
+    assert (rec["host_results"], rec["waves_released"], rec["fenced"]) == (0, 0, 0), rec
     assert np.array_equal(to_host(db), exp)
 
 
@@ -1233,6 +1246,11 @@ def test_recovery_finish_matches_two_step(gpu, oracle, kind):
             else:
                 rec.add_peer(2, buf(data[2], in_kind))
                 rec.solve({}, {1: o})
+            sync = ec.last_sync()
+            if out_kind == "pinned":  # the kernel wrote host memory: fenced before return
+                assert sync["host_results"] == 1 and sync["fenced"] == 1, sync
+            elif out_kind == "device":
+                assert sync["host_results"] == 0 and sync["fenced"] == 0, sync
             assert rec.complete
             torch.cuda.synchronize()
             outs.append(o.cpu().numpy() if hasattr(o, "cpu") else o)
@@ -1364,6 +1382,8 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                     done = []
             assert pool.active == 0
             if out_kind == "pinned":  # read on return of the last synchronous call
+                sync = ec.last_sync()
+                assert sync["host_results"] == 1 and sync["fenced"] == 1, sync
                 assert np.array_equal(out0.numpy(), data[0])
         torch.cuda.synchronize()
         assert np.array_equal(to_host(out0), data[0])

@@ -139,5 +139,12 @@ s)
   # hot path compiled to) against the scalar-base form the library uses
   timeout -k 10 200 tools/small_batch_probe.bin 20 > gpurun_out/r03s/small_batch_probe_vaddr2.jsonl 2>&1
   ;;
+t)
+  # round-3 (second session): the completion-protocol assertions (cec_last_sync) in the GPU
+  # suite on a fresh build, smoke, and the default bench line
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03t/pytest.log 2>&1 && \
+  timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03t/smoke.log 2>&1 && \
+  timeout -k 10 600 python -u bench.py > gpurun_out/r03t/bench_default.jsonl 2> gpurun_out/r03t/bench_default.err
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
