@@ -146,5 +146,19 @@ t)
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03t/smoke.log 2>&1 && \
   timeout -k 10 600 python -u bench.py > gpurun_out/r03t/bench_default.jsonl 2> gpurun_out/r03t/bench_default.err
   ;;
+u)
+  # round-3 (second session): LDS engine, two 128-lane workgroups per tile for launches
+  # staging >= 3 product rows (the rotating decode), else four 64-lane (the encode):
+  # LDS-engine GPU tests, then the LDS line + diff-update and --ops against the previous
+  # choice pinned by CEC_SPLIT_SHIFT=2
+  run pytest_lds 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "lds or golden or fuzz or decode"
+  B="python -u bench.py --engine lds --also=rs32_diff_update --no-cpu-baseline --no-strong"
+  for i in 1 2 3; do
+    run lds_new_$i 200 $B
+    run lds_s2_$i 200 env CEC_SPLIT_SHIFT=2 $B
+  done
+  run ops_new 200 python -u bench.py --ops --engine lds
+  run ops_s2 200 env CEC_SPLIT_SHIFT=2 python -u bench.py --ops --engine lds
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
