@@ -160,5 +160,10 @@ u)
   run ops_new 200 python -u bench.py --ops --engine lds
   run ops_s2 200 env CEC_SPLIT_SHIFT=2 python -u bench.py --ops --engine lds
   ;;
+v)
+  # round-3 (second session): load policy at the strong-scaling shares (memory-side cache
+  # reuse between the encode and the decode), bare XOR streams with write-through stores
+  timeout -k 10 200 tools/small_batch_probe.bin 20 loads > gpurun_out/r03v/small_batch_loads.jsonl 2>&1
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac

@@ -13,12 +13,18 @@
 //   sc1nt   raw buffer store, aux 18
 // and prints per size and policy the median encode / decode us and, per policy, the
 // fixed cost a of t(stripes) = a + b * stripes fitted from 8,192 and 65,536.
+// `small_batch_probe.bin STEPS loads`: the load policy instead, with write-through stores
+// (the library's store at these shares): does a load that may allocate in the
+// memory-side cache let the decode re-read what the encode just read / wrote (the whole
+// working set of an 8,192-stripe share is 256 MiB)?  Loads: nt (the library's), or a raw
+// buffer load with aux 0 (default), 1 (sc0), 16 (sc1), 17 (sc0 sc1).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/small_batch_probe.hip -o tools/small_batch_probe.bin
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #define CK(x)                                                              \
@@ -54,7 +60,17 @@ __device__ inline void store16(uint8_t *base, uint32_t bytes, uint32_t off, u32x
 // the start of a launch) is a per-launch cost.  kMode 2: no cold path, but every load
 // and nt store through a 64-bit vector address instead of a scalar base + 32-bit vector
 // offset (what kMode 1's hot path compiled to), to separate the addressing form.
-template <int W, int AUX, int kMode = 0>
+template <int LAUX>
+__device__ inline u32x4 load16(const uint8_t *base, uint32_t bytes, uint32_t off) {
+    if constexpr (LAUX < 0) {
+        return __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)base + off));
+    } else {
+        auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(base), 0, bytes, 0x00020000);
+        return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, LAUX);
+    }
+}
+
+template <int W, int AUX, int kMode = 0, int LAUX = -1>
 __global__ __launch_bounds__(64) void k_stream(Args a) {
     const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
     u32x4 acc = {0, 0, 0, 0};
@@ -72,9 +88,13 @@ __global__ __launch_bounds__(64) void k_stream(Args a) {
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const GL u32x4 *p = (const GL u32x4 *)((uintptr_t)a.r[i] + off);
-        if constexpr (kMode == 2) asm volatile("" : "+v"(p));
-        acc ^= __builtin_nontemporal_load(p);
+        if constexpr (LAUX >= 0) {
+            acc ^= load16<LAUX>(a.r[i], a.bytes, off);
+        } else {
+            const GL u32x4 *p = (const GL u32x4 *)((uintptr_t)a.r[i] + off);
+            if constexpr (kMode == 2) asm volatile("" : "+v"(p));
+            acc ^= __builtin_nontemporal_load(p);
+        }
     }
 #pragma unroll
     for (int j = 0; j < W; ++j) {
@@ -99,7 +119,7 @@ __global__ void k_fill(uint64_t *p, uint64_t n, uint64_t seed) {
     }
 }
 
-template <int AUX, int kMode = 0>
+template <int AUX, int kMode = 0, int LAUX = -1>
 static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps, double fit[2][2]) {
     const uint32_t sizes[] = {8192, 16384, 65536};
     for (uint32_t stripes : sizes) {
@@ -110,15 +130,15 @@ static void run(const char *name, uint8_t *const *ar, uint64_t stride, int steps
         std::vector<hipEvent_t> ev(2 * steps + 1);
         for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
         for (int w = 0; w < 3; ++w) {
-            k_stream<2, AUX, kMode><<<grid, 64>>>(enc);
-            k_stream<1, AUX, kMode><<<grid, 64>>>(dec);
+            k_stream<2, AUX, kMode, LAUX><<<grid, 64>>>(enc);
+            k_stream<1, AUX, kMode, LAUX><<<grid, 64>>>(dec);
         }
         CK(hipDeviceSynchronize());
         CK(hipEventRecord(ev[0], 0));
         for (int s = 0; s < steps; ++s) {
-            k_stream<2, AUX, kMode><<<grid, 64>>>(enc);
+            k_stream<2, AUX, kMode, LAUX><<<grid, 64>>>(enc);
             CK(hipEventRecord(ev[2 * s + 1], 0));
-            k_stream<1, AUX, kMode><<<grid, 64>>>(dec);
+            k_stream<1, AUX, kMode, LAUX><<<grid, 64>>>(dec);
             CK(hipEventRecord(ev[2 * s + 2], 0));
         }
         CK(hipDeviceSynchronize());
@@ -163,7 +183,16 @@ int main(int argc, char **argv) {
     }
     CK(hipDeviceSynchronize());
     double fit[2][2];
-    for (int rep = 0; rep < 2; ++rep) {  // two passes: policy order effects show up
+    const bool loads = argc > 2 && !strcmp(argv[2], "loads");
+    for (int rep = 0; loads && rep < 3; ++rep) {
+        run<16, 0, -1>("sc1_ld_nt", ar, stride, steps, fit);
+        run<16, 0, 0>("sc1_ld_plain", ar, stride, steps, fit);
+        run<16, 0, 1>("sc1_ld_sc0", ar, stride, steps, fit);
+        run<16, 0, 16>("sc1_ld_sc1", ar, stride, steps, fit);
+        run<16, 0, 17>("sc1_ld_sc0sc1", ar, stride, steps, fit);
+        run<-1, 0, 0>("nt_ld_plain", ar, stride, steps, fit);
+    }
+    for (int rep = 0; !loads && rep < 2; ++rep) {  // two passes: policy order effects show up
         run<-1>("nt", ar, stride, steps, fit);
         run<0>("plain", ar, stride, steps, fit);
         run<16>("sc1", ar, stride, steps, fit);
