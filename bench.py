@@ -321,8 +321,17 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     k, m, n, _, what = WORKLOADS[workload]
     stripes, arena = layout(workload)
     full_bytes = sum(ln for _, ln in stripes)
+    full_arena = arena
     if share is not None:
         stripes, arena = share_layout(stripes, *share)
+        # A GPU's arenas keep the whole batch's size and its share fills their start: a
+        # Cocytus server's arenas are MEMSIZE whatever number of values its key shard
+        # receives (const.h:25, memcached.c:380-381), so only the values per GPU change
+        # with N.  (Share-sized arenas, CEC_BENCH_SHARE_ARENA=share, put the streams
+        # 32 MiB apart at 8,192 stripes: encode 28.3-28.7 against 27.6-28.1 us,
+        # profiles/r03_evidence/share_arena_ab/.)
+        if os.environ.get("CEC_BENCH_SHARE_ARENA") != "share":
+            arena = full_arena
     B = len(stripes)
     mat = ec.coding_matrix(k, m)
     g = torch.Generator(device="cuda").manual_seed(0xC0C70002 + rank)

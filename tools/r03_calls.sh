@@ -165,5 +165,19 @@ v)
   # reuse between the encode and the decode), bare XOR streams with write-through stores
   timeout -k 10 200 tools/small_batch_probe.bin 20 loads > gpurun_out/r03v/small_batch_loads.jsonl 2>&1
   ;;
+w)
+  # round-3 (second session): kernel-argument size and the slot-table chain at the
+  # strong-scaling shares (the library's argument form on the bare stream)
+  timeout -k 10 200 tools/small_batch_probe.bin 20 kernarg > gpurun_out/r03w/small_batch_kernarg.jsonl 2>&1
+  ;;
+x)
+  # round-3 (second session): arena size at the strong-scaling shares -- share-sized arenas
+  # (32 MiB + 4 KiB apart at 8,192 stripes) against arenas of the whole batch's size (the
+  # bare-stream probe's spacing, 256 MiB + 4 KiB), same build, interleaved
+  for i in 1 2 3; do
+    run share_$i 200 python -u bench.py --also= --no-cpu-baseline
+    run batch_$i 200 env CEC_BENCH_SHARE_ARENA=batch python -u bench.py --also= --no-cpu-baseline
+  done
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac

@@ -45,6 +45,17 @@ struct Args {
     uint32_t bytes;  // per arena (buffer descriptors' range)
 };
 
+// `small_batch_probe.bin STEPS kernarg`: the library's kernel-argument form at these shares.
+// BigArgs is as large as the library's (48 stream slots + table pointers, 440 B);
+// kMode 3 reads its streams at fixed slots, kMode 4 through slot numbers loaded from a
+// small table in global memory first (the library's tile -> pattern -> stream chain).
+struct BigArgs {
+    uint8_t *base[48];
+    const uint8_t *slots;  // kMode 4: in slots 0-2, out slots 3-4
+    uint64_t pad[6];
+    uint32_t bytes;
+};
+
 template <int AUX>
 __device__ inline void store16(uint8_t *base, uint32_t bytes, uint32_t off, u32x4 v) {
     if constexpr (AUX < 0) {
@@ -107,6 +118,72 @@ __global__ __launch_bounds__(64) void k_stream(Args a) {
         } else {
             store16<AUX>(a.w[j], a.bytes, off, v);
         }
+    }
+}
+
+template <int W, int kMode>
+__global__ __launch_bounds__(64) void k_stream_big(BigArgs a) {
+    const uint32_t off = blockIdx.x * 1024u + threadIdx.x * 16u;
+    int si[5] = {0, 1, 2, 3, 4};
+    if constexpr (kMode == 4) {
+        const __attribute__((address_space(4))) uint8_t *t =
+            (const __attribute__((address_space(4))) uint8_t *)(uintptr_t)a.slots;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) si[i] = t[i];
+    }
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+        acc ^= __builtin_nontemporal_load((const GL u32x4 *)((uintptr_t)a.base[si[i]] + off));
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+        u32x4 v = acc;
+        v.x ^= j;
+        store16<16>(a.base[si[3 + j]], a.bytes, off, v);
+    }
+}
+
+template <int kMode>
+static void run_big(const char *name, uint8_t *const *ar, const uint8_t *d_slots_enc,
+                    const uint8_t *d_slots_dec, int steps) {
+    const uint32_t sizes[] = {8192, 16384, 65536};
+    for (uint32_t stripes : sizes) {
+        const uint32_t bytes = stripes * 4096u;
+        BigArgs enc{}, dec{};
+        // slot layout as the library's: data 0-2, parity 3-4, rebuilt 5
+        for (int i = 0; i < 6; ++i) enc.base[i] = dec.base[i] = ar[i];
+        enc.slots = d_slots_enc;
+        dec.slots = d_slots_dec;
+        enc.bytes = dec.bytes = bytes;
+        if (kMode == 3) {  // fixed slots: the decode reads 1, 2, 3 and writes 5
+            dec.base[0] = ar[1]; dec.base[1] = ar[2]; dec.base[2] = ar[3]; dec.base[3] = ar[5];
+        }
+        const dim3 grid(stripes * 4);
+        std::vector<hipEvent_t> ev(2 * steps + 1);
+        for (auto &e : ev) CK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
+        for (int w = 0; w < 3; ++w) {
+            k_stream_big<2, kMode><<<grid, 64>>>(enc);
+            k_stream_big<1, kMode><<<grid, 64>>>(dec);
+        }
+        CK(hipDeviceSynchronize());
+        CK(hipEventRecord(ev[0], 0));
+        for (int s = 0; s < steps; ++s) {
+            k_stream_big<2, kMode><<<grid, 64>>>(enc);
+            CK(hipEventRecord(ev[2 * s + 1], 0));
+            k_stream_big<1, kMode><<<grid, 64>>>(dec);
+            CK(hipEventRecord(ev[2 * s + 2], 0));
+        }
+        CK(hipDeviceSynchronize());
+        std::vector<float> te(steps), td(steps);
+        for (int s = 0; s < steps; ++s) {
+            CK(hipEventElapsedTime(&te[s], ev[2 * s], ev[2 * s + 1]));
+            CK(hipEventElapsedTime(&td[s], ev[2 * s + 1], ev[2 * s + 2]));
+        }
+        std::sort(te.begin(), te.end());
+        std::sort(td.begin(), td.end());
+        printf("{\"policy\": \"%s\", \"stripes\": %u, \"encode_us\": %.2f, \"decode_us\": %.2f}\n", name,
+               stripes, 1e3 * te[steps / 2], 1e3 * td[steps / 2]);
+        for (auto &e : ev) CK(hipEventDestroy(e));
     }
 }
 
@@ -184,6 +261,22 @@ int main(int argc, char **argv) {
     CK(hipDeviceSynchronize());
     double fit[2][2];
     const bool loads = argc > 2 && !strcmp(argv[2], "loads");
+    if (argc > 2 && !strcmp(argv[2], "kernarg")) {
+        const uint8_t h_enc[8] = {0, 1, 2, 3, 4, 0, 0, 0}, h_dec[8] = {1, 2, 3, 5, 5, 0, 0, 0};
+        uint8_t *d_slots;
+        CK(hipMalloc(&d_slots, 16));
+        CK(hipMemcpy(d_slots, h_enc, 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(d_slots + 8, h_dec, 8, hipMemcpyHostToDevice));
+        double fit[2][2];
+        for (int rep = 0; rep < 3; ++rep) {
+            run<16>("sc1", ar, stride, steps, fit);
+            run_big<3>("sc1_bigargs", ar, d_slots, d_slots + 8, steps);
+            run_big<4>("sc1_bigargs_slot_table", ar, d_slots, d_slots + 8, steps);
+        }
+        CK(hipFree(d_slots));
+        CK(hipFree(slab));
+        return 0;
+    }
     for (int rep = 0; loads && rep < 3; ++rep) {
         run<16, 0, -1>("sc1_ld_nt", ar, stride, steps, fit);
         run<16, 0, 0>("sc1_ld_plain", ar, stride, steps, fit);
