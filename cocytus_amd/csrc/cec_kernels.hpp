@@ -284,6 +284,15 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 // work item g is tile g >> split_shift, part g & (2^split_shift - 1).
 // kSysRel: every wave ends with a system-scope release (kFlagSysRelease launches; a
 // template parameter, so the batched kernels carry no epilogue at all).
+// LDS engine, full aligned tiles: stage the product rows before the stream loads (the
+// fast path in combine_kernel) for the diff-update shapes only (2 inputs, parity
+// read-modify-write).  There it ran the diff-update + install 3.5 % faster; in the
+// encode (3 x 2) the second path's registers cost SGPR spills and occupancy (+10 %),
+// and the fixed-mask decode / residual (3 x 1) lost 2-3 %
+// (profiles/r03_evidence/lds_early_rows/).
+template <int NT, int kAcc, bool kExact>
+constexpr bool kEarlyRows = kExact && NT == 2 && (kAcc == kAccAll || kAcc == kAccAllButLast);
+
 template <int NT, int LT, class Eng, int kAcc, bool kExact, int S = kMaxStreams, bool kSysRel = false>
 __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
     extern __shared__ uint4 cec_lds_rows[];  // LDS engine: the pattern's product rows
@@ -339,6 +348,42 @@ __global__ __launch_bounds__(kBlock) void combine_kernel(CombineArgsN<S> a) {
         // rarely a multiple of 16) and tiles of misaligned device pointers use the
         // branch-free byte gather / scatter, everything else dwordx4.
         const uint32_t pos = lane * 16;
+        if constexpr (Eng::kStaged && kEarlyRows<NT, kAcc, kExact>) {
+            if ((mis & 15) == 0 && tr.len == kTile) {
+                // A full, aligned tile (wave-uniform: every lane one whole chunk), the
+                // LDS engine's common case.  Its product rows are fetched BEFORE the
+                // stream loads, and the stream loads are unconditional, so the LDS write
+                // waits only for the rows (vmcnt counts loads in order) and the write
+                // and the barrier complete under the streams' HBM latency; the lookups
+                // start as soon as the stream data lands.  (Staged after the stream
+                // loads, below, the write waits for every stream load.)
+                const uint32_t nb16 = static_cast<uint32_t>(P->lds_rows) * 16u;
+                const uint4 *row_src = reinterpret_cast<const uint4 *>(a.rows) + P->lds_row_base * 16;
+                uint4 row0 = make_uint4(0, 0, 0, 0);
+                if (threadIdx.x < nb16) row0 = row_src[threadIdx.x];
+                uint4 x[NT];
+                uint4 acc[LT];
+#pragma unroll
+                for (int i = 0; i < NT; ++i)
+                    if (i < n_in) x[i] = ld16(in[i], pos);
+#pragma unroll
+                for (int l = 0; l < LT; ++l) {
+                    acc[l] = make_uint4(0, 0, 0, 0);
+                    if (l < n_out && is_acc(l)) acc[l] = ld16(out[l], pos);
+                }
+                if (nb16) {
+                    if (threadIdx.x < nb16) cec_lds_rows[threadIdx.x] = row0;
+                    for (uint32_t b = threadIdx.x + blockDim.x; b < nb16; b += blockDim.x)
+                        cec_lds_rows[b] = row_src[b];  // (more rows than lanes)
+                    __syncthreads();
+                }
+                compute_chunk<NT, LT, Eng>(P, n_in, n_out, x, acc, lds);
+#pragma unroll
+                for (int l = 0; l < LT; ++l)
+                    if (l < n_out) st16(out[l], pos, acc[l]);
+                continue;
+            }
+        }
         const bool active = pos < tr.len;
         if constexpr (!Eng::kStaged)
             if (!active) continue;  // (staged engines keep every lane to the barrier)

@@ -179,5 +179,30 @@ x)
     run batch_$i 200 env CEC_BENCH_SHARE_ARENA=batch python -u bench.py --also= --no-cpu-baseline
   done
   ;;
+y)
+  # round-3 (second session): LDS engine, full aligned tiles stage their product rows
+  # before the stream loads (the LDS write and barrier under the HBM latency) -- LDS GPU
+  # tests, then the LDS line + diff-update against the previous build (tools/ab_prev)
+  run pytest_lds 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "lds or golden or fuzz or decode"
+  B="python -u bench.py --engine lds --also=rs32_diff_update --no-cpu-baseline --no-strong"
+  for i in 1 2 3; do
+    run lds_new_$i 200 $B
+    run lds_prev_$i 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so $B
+  done
+  run ops_new 200 python -u bench.py --ops --engine lds
+  run ops_prev 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u bench.py --ops --engine lds
+  ;;
+z)
+  # round-3 (second session): early row staging restricted to the diff-update shapes --
+  # LDS GPU tests, then the LDS line + diff-update against the previous build
+  run pytest_lds 700 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -k "lds or golden or fuzz or diff"
+  B="python -u bench.py --engine lds --also=rs32_diff_update --no-cpu-baseline --no-strong"
+  for i in 1 2 3; do
+    run lds_new_$i 200 $B
+    run lds_prev_$i 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so $B
+  done
+  run ops_new 200 python -u bench.py --ops --engine lds
+  run ops_prev 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u bench.py --ops --engine lds
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
