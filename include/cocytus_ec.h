@@ -343,8 +343,9 @@ int cec_cache_trim(void);
 
 /* ---- completion record (diagnostics) ----
  * How the calling thread's last synchronous completion (the drop-in
- * galois_w08_region_multiply, cec_recovery_fold_update / _solve / _finish, the pool's
- * flush_solve / solve) made its results visible to the host on return.  A result in
+ * galois_w08_region_multiply, cec_recovery_fold_update / _solve / _finish,
+ * cec_recovery_pool_flush / _flush_solve / _fold_update / _solve) made its results
+ * visible to the host on return.  A result in
  * host-visible memory (pinned, mapped or managed) may still sit in the L2 of the XCD
  * that wrote it; it is visible only if every writing wave ended with a system-scope
  * release or a system-scope fence ran behind the op.  Tests assert the protocol with it
