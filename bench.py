@@ -60,6 +60,9 @@ EXTRA_WORKLOADS = {
                 "(H2D -> kernels -> D2H pipelined over HIP streams)",
     "rs32_4k_lds": "the metric's workload with the LDS engine: GF(2^8) products from 256-entry "
                    "log/antilog product rows staged in LDS (the north star's named kernel form)",
+    "rs32_1m_recovery": "BASELINE configs[4] as stated: online recovery decode of ONE lost data shard "
+                        "(every stripe the same), 1,024 x 1 MiB values, device-resident; D0 led by P0 "
+                        "(inverse 1) and D1 led by P1 (inverse 1/245), SURVEY §8d",
 }
 
 
@@ -85,7 +88,8 @@ def parse(argv=None):
     ap.add_argument("--harness-check", action="store_true",
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
-    ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_diff_update,rs32_e2e",
+    ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_1m_recovery,"
+                                      "rs32_diff_update,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -545,6 +549,64 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
     }
 
 
+def measure_recovery_decode(torch, dist, ec, world, rank, args):
+    """BASELINE configs[4] as SURVEY §8d states it: RS(3,2) decode of one lost data shard,
+    1,024 x 1 MiB values, one fixed mask for the whole batch (a recovering server rebuilds
+    one lid, memcached.c:7842-7922): D0 led by P0 (inverse 1) and D1 led by P1 (inverse
+    1/245), each timed as args.steps back-to-back cec_decode launches of the whole batch.
+    value = rebuilt GiB/s (n per stripe), per case; check: the rebuilt shard == the data."""
+    k, m, n, B = 3, 2, 1 << 20, 1024
+    T = n * B
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70005 + rank)
+    ar = ec.arena_tensors(k + m + 1, T)
+    data, parity, out = ar[:k], ar[k:k + m], ar[k + m]
+    for t in data:
+        t.random_(0, 256, generator=g)
+    stream = torch.cuda.current_stream()
+    ec.encode_region(k, m, mat, data, parity, T, stream)
+    plan = ec.Plan([(s * n, 0, n, 0) for s in range(B)])
+    cases = {}
+    for name, lost, leader in (("D0_leader_P0", 0, k), ("D1_leader_P1", 1, k + 1)):
+        mask = ec.recovery_mask(k, m, leader, [int(i != lost) for i in range(k + m)])
+        outs = [out if j == lost else None for j in range(k)]
+        out.zero_()
+        for _ in range(args.warmup):
+            ec.decode(k, m, mat, [mask], data + parity, outs, plan, stream)
+        evs = [ec.Event() for _ in range(args.steps + 1)]
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        evs[0].record(stream)
+        for s in range(args.steps):
+            ec.decode(k, m, mat, [mask], data + parity, outs, plan, stream)
+            evs[s + 1].record(stream)
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            dist.barrier()
+        ts = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
+        ms = sum(ts) / args.steps
+        ok = bool(torch.equal(out, data[lost]))
+        elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist)
+        dec_bytes = (k + 1) * T  # read K survivors, write the rebuilt shard
+        gbps = dec_bytes / (ms * 1e-3) / 1e9
+        cases[name] = {
+            "value": round(n * B * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s rebuilt",
+            "mask": mask, "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(ts), 4),
+            "decode_frac": round(gbps / HBM_PEAK_GBPS, 4), "achieved_GBps": round(gbps, 1),
+            "algorithmic_bytes_per_launch": dec_bytes, "verified": ok and bad == 0.0,
+        }
+    plan.destroy()
+    del ar, data, parity, out
+    return {"workload": EXTRA_WORKLOADS["rs32_1m_recovery"], "cases": cases,
+            "value": min(c["value"] for c in cases.values()), "unit": "GiB/s rebuilt (slower case)",
+            "decode_frac": min(c["decode_frac"] for c in cases.values()),
+            "verified": all(c["verified"] for c in cases.values())}
+
+
 def pcie_raw(torch, nbytes=256 << 20, reps=4):
     """Raw pinned H2D / D2H copy rates of this GPU's link (GB/s)."""
     x = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -684,6 +746,9 @@ def run_device(args):
             continue
         if w == "rs32_e2e":
             also[w] = measure_e2e(torch, dist, ec, world, rank, args)
+            continue
+        if w == "rs32_1m_recovery":
+            also[w] = measure_recovery_decode(torch, dist, ec, world, rank, args)
             continue
         engine = args.engine
         if w == "rs32_4k_lds":

@@ -220,5 +220,11 @@ san2)
   timeout -k 10 600 bash tools/asan.sh run > gpurun_out/r03san2/asan.txt 2>&1 && \
   timeout -k 10 600 bash tools/tsan.sh run > gpurun_out/r03san2/tsan.txt 2>&1
   ;;
+rec)
+  # round-3 (second session): configs[4] as stated (fixed-mask recovery decode, 1 MiB values)
+  run rec1 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong
+  run rec2 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine lds
+  run pytest2 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "two_ranks"
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
