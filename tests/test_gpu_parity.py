@@ -1332,6 +1332,12 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                 else torch.zeros(nunits * U, dtype=torch.uint8, device="cuda"))
         mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])  # D0 lost, leader P0
         pending, done = {}, []  # id -> (ub, ue, peers left)
+
+        def check_sync():  # a solve into pinned memory is fenced before it returns; HBM: not
+            sync = ec.last_sync()
+            want = (1, 1) if out_kind == "pinned" else (0, 0)
+            assert (sync["host_results"], sync["fenced"]) == want, (out_kind, sync)
+
         next_unit, window = 0, 24
         with ec.RecoveryPool(k, m, mat, 3, p0, capacity_units=64) as pool:
             while next_unit < nunits or pending:
@@ -1358,6 +1364,7 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                         pool.flush()
                     else:  # the completed single-loss requests are rebuilt in the same pass
                         pool.flush_solve([out0, None, None])
+                        check_sync()
                 if rng.random() < 0.25:  # a SET on a surviving data shard lands
                     j = int(rng.integers(1, 3))
                     ln = int(rng.integers(1, 9000))
@@ -1377,13 +1384,12 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                         done.append(rid)
                 if done and (rng.random() < 0.3 or not pending):
                     pool.solve(done, [out0, None, None])
+                    check_sync()
                     for d in done:
                         pool.end(d)
                     done = []
             assert pool.active == 0
             if out_kind == "pinned":  # read on return of the last synchronous call
-                sync = ec.last_sync()
-                assert sync["host_results"] == 1 and sync["fenced"] == 1, sync
                 assert np.array_equal(out0.numpy(), data[0])
         torch.cuda.synchronize()
         assert np.array_equal(to_host(out0), data[0])
