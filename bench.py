@@ -60,6 +60,8 @@ EXTRA_WORKLOADS = {
                 "(H2D -> kernels -> D2H pipelined over HIP streams)",
     "rs32_4k_lds": "the metric's workload with the LDS engine: GF(2^8) products from 256-entry "
                    "log/antilog product rows staged in LDS (the north star's named kernel form)",
+    "rs32_diff_update_lds": "the per-SET diff-update + install with the LDS engine (the north star's "
+                            "first op in its named form)",
     "rs32_1m_recovery": "BASELINE configs[4] as stated: online recovery decode of ONE lost data shard "
                         "(every stripe the same), 1,024 x 1 MiB values, device-resident; D0 led by P0 "
                         "(inverse 1) and D1 led by P1 (inverse 1/245), SURVEY §8d",
@@ -89,7 +91,7 @@ def parse(argv=None):
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
     ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_1m_recovery,"
-                                      "rs32_diff_update,rs32_e2e",
+                                      "rs32_diff_update,rs32_diff_update_lds,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -527,6 +529,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         dist.barrier()
     du_t = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
     ms = sum(du_t) / args.steps
+    lds = ec.get_engine() == ec.CEC_ENGINE_LDS
     chk = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
     ec.encode_region(k, m, mat, data, chk, T, stream)
     torch.cuda.synchronize()
@@ -543,8 +546,12 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         "roofline": {"bound": "hbm", "achieved": round(gbps, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                      "frac": round(gbps / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": nbytes,
                      "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(du_t), 4),
-                     "kernel": "combine_kernel<2,3,*,kAccAllButLast,exact> (cec_diff_update, install)",
-                     "traffic": load_traffic("rs32_diff_update", ("diff_update",))[0]},
+                     "kernel": f"combine_kernel<2,3,{'LdsEngine' if lds else 'PermEngine'},kAccAllButLast,exact> "
+                               "(cec_diff_update, install)",
+                     # (profiles/pmc_traffic.json holds the default engine's passes; the LDS
+                     # engine's are in profiles/r03s2_lds_summary.md)
+                     "traffic": None if lds else load_traffic("rs32_diff_update", ("diff_update",))[0]},
+        "engine": "lds" if lds else "perm",
         "verified": bool(ok and bad == 0.0),
     }
 
@@ -741,8 +748,13 @@ def run_device(args):
     also = {}
     for w in [x for x in args.also.split(",") if x and x != args.workload]:
         torch.cuda.empty_cache()
-        if w == "rs32_diff_update":
-            also[w] = measure_diff_update(torch, dist, ec, world, rank, args)
+        if w in ("rs32_diff_update", "rs32_diff_update_lds"):
+            if w == "rs32_diff_update_lds":
+                ec.set_engine(ec.CEC_ENGINE_LDS)
+            try:
+                also[w] = measure_diff_update(torch, dist, ec, world, rank, args)
+            finally:
+                ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
             continue
         if w == "rs32_e2e":
             also[w] = measure_e2e(torch, dist, ec, world, rank, args)

@@ -247,10 +247,12 @@ struct Streams {
     uint8_t *base[kMaxStreams] = {};
 };
 
-// One launch over a tile source (plan or implicit region) with a pattern set.
+// One launch over a tile source (plan or implicit region) with a pattern set built for
+// `engine` (the patterns' coefficient form and the kernel must agree: the engine is read
+// once per op, so a concurrent cec_set_engine cannot split them).
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
-                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used);
+                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used, int engine);
 
 // ============================================================== plans
 // Tiles of one extent end on 4 KiB boundaries of the arena offset, so interior
@@ -534,7 +536,7 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
 
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
-                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used) {
+                       uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used, int engine) {
     uint64_t n_tiles;
     if (plan) {
         if (plan->device != dev)
@@ -553,7 +555,7 @@ static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &p
     key.append(reinterpret_cast<const char *>(rows.data()), rows.size());
     PatEntry *entry = nullptr;
     if (int r = pattern_get(dev, std::move(key), stream, &entry)) return r;
-    const int rc = launch_combine(dev, st, entry->d, pats.size(), sh, g_engine.load() == CEC_ENGINE_LDS, plan,
+    const int rc = launch_combine(dev, st, entry->d, pats.size(), sh, engine == CEC_ENGINE_LDS, plan,
                                   implicit_len, n_tiles, stream, pats.data(), used);
     // the plan's streams, for its destroy (host-side only); the tables may be evicted
     // again once the launch is enqueued (eviction synchronises the device)
@@ -618,7 +620,7 @@ static int run_combos(int dev, const Streams &st, const std::vector<Combo> &comb
         std::vector<Pattern> pats;
         std::vector<uint8_t> rows;
         build_patterns(combos, g, engine, pats, rows);
-        if (int r = run_combine(dev, st, pats, rows, plan, implicit_len, stream, used)) return r;
+        if (int r = run_combine(dev, st, pats, rows, plan, implicit_len, stream, used, engine)) return r;
     }
     return CEC_OK;
 }

@@ -347,3 +347,57 @@ def test_caches_under_concurrent_threads(gpu, tmp_path):
     out = run_cache_threads(tmp_path, threads=8, iters=60, limit=6)
     assert out["bad"] == 0 and out["errors"] == 0 and out["checks"] == 8 * 60 * 49
     assert out["evictions"] > 0
+
+
+def test_engine_switch_under_concurrent_ops(gpu, oracle):
+    """cec_set_engine is process-wide: another thread may switch it while an op runs.
+    Each op reads the engine once, so its coefficient tables and its kernel always agree
+    (PERM tables under the LDS kernel, or the reverse, would give wrong bytes).  One
+    thread flips the engine as fast as it can while this one encodes, diff-updates and
+    multiplies regions on its own stream; every result is checked."""
+    import threading
+
+    torch, ec = gpu
+    k, m, n, B = 3, 2, 4096, 64
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xE1)
+    host = [rng.integers(0, 256, B * n, dtype=np.uint8) for _ in range(k)]
+    exp_par = oracle.encode(mat, k, m, host)
+    data = [torch.from_numpy(h).cuda() for h in host]
+    parity = [torch.zeros(B * n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    src = rng.integers(0, 256, 3 * n + 5, dtype=np.uint8)
+    base = rng.integers(0, 256, 3 * n + 5, dtype=np.uint8)
+    exp_rm = base.copy()
+    oracle.region_multiply(src, 0x53, exp_rm, 1)
+    dsrc = torch.from_numpy(src).cuda()
+    default = ec.get_engine()
+    stop = threading.Event()
+    flips = [0]
+
+    def flipper():
+        e = 0
+        while not stop.is_set():
+            e ^= 1
+            ec.set_engine(ec.CEC_ENGINE_LDS if e else ec.CEC_ENGINE_PERM)
+            flips[0] += 1
+
+    t = threading.Thread(target=flipper)
+    s = torch.cuda.Stream()
+    t.start()
+    try:
+        with ec.Plan([(i * n, 0, n, 0) for i in range(B)]) as plan, torch.cuda.stream(s):
+            for it in range(150):
+                for p in parity:
+                    p.zero_()
+                ec.encode(k, m, mat, data, parity, plan, s)
+                dst = torch.from_numpy(base.copy()).cuda()
+                ec.region_multiply(dsrc, 0x53, src.size, dst, 1, s)
+                s.synchronize()
+                for p in range(m):
+                    assert np.array_equal(parity[p].cpu().numpy(), exp_par[p]), (it, p)
+                assert np.array_equal(dst.cpu().numpy(), exp_rm), it
+    finally:
+        stop.set()
+        t.join()
+        ec.set_engine(default)
+    assert flips[0] > 150

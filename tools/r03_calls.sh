@@ -232,5 +232,23 @@ q2)
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03q2/smoke.log 2>&1 && \
   s0=$SECONDS && timeout -k 10 600 python -u bench.py > gpurun_out/r03q2/bench_default.jsonl 2> gpurun_out/r03q2/bench_default.err && echo "bench wall $((SECONDS - s0)) s" > gpurun_out/r03q2/bench_wall.txt
   ;;
+du2)
+  # round-3 (second session): the pool test's per-call completion checks, the default line
+  # with the LDS diff-update beside the default engine's
+  run pytest_pool 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 240 --timeout-method thread -k "pool or two_ranks"
+  run bench 300 python -u bench.py
+  ;;
+eng)
+  # round-3 (second session): the engine read once per op -- the concurrent engine-switch
+  # test on this build, then on the previous build (tools/ab_prev, engine read twice; a
+  # mismatch gives wrong bytes, never a fault: LDS reads past the allocation return 0)
+  run pytest_eng 300 python -u -m pytest tests/test_gpu_runtime.py -x -q --timeout 240 --timeout-method thread -k "engine_switch"
+  timeout -k 10 300 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u -m pytest tests/test_gpu_runtime.py -x -q --timeout 240 --timeout-method thread -k "engine_switch" > gpurun_out/r03eng/pytest_eng_prev.log 2>&1; echo "prev rc=$?"
+  run pytest_rt 600 python -u -m pytest tests/test_gpu_runtime.py tests/test_gpu_golden.py -x -q --timeout 240 --timeout-method thread
+  ;;
+engprev)
+  # the negative control of case eng alone (tools/ab_prev uploaded for this call)
+  timeout -k 10 300 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u -m pytest tests/test_gpu_runtime.py -x -q --timeout 240 --timeout-method thread -k "engine_switch" > gpurun_out/r03engprev/pytest_eng_prev.log 2>&1; echo "prev rc=$?"
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
