@@ -22,6 +22,14 @@
  * a handle of a destroyed stream cannot be synchronised (it crashes the HIP runtime).
  * This is a change from the first release, whose destroy waited for the whole device.
  *
+ * THREADS: every entry point may be called from any thread.  The library's shared
+ * state (caches, the engine and occupancy settings) is thread-safe, and each op reads
+ * the process-wide engine once, so a concurrent cec_set_engine changes later ops only.
+ * A plan is immutable once created and may be used by several threads' ops at once.
+ * Drainers, recovery sessions and recovery pools carry per-object state: calls on one
+ * such object must not overlap (one thread at a time, as Cocytus' single worker thread
+ * per process makes them).
+ *
  * Coding matrix: int[(k+m)*k], row-major, MATRIX(x,y) = matrix[x*k+y]
  * (/root/reference/memcached.h:52), as returned by
  * reed_sol_big_vandermonde_distribution_matrix(k+m, k, 8)
