@@ -60,8 +60,8 @@ EXTRA_WORKLOADS = {
                 "(H2D -> kernels -> D2H pipelined over HIP streams)",
     "rs32_4k_lds": "the metric's workload with the LDS engine: GF(2^8) products from 256-entry "
                    "log/antilog product rows staged in LDS (the north star's named kernel form)",
-    "rs32_diff_update_lds": "the per-SET diff-update + install with the LDS engine (the north star's "
-                            "first op in its named form)",
+    "rs32_diff_update_perm": "the per-SET diff-update + install with the PERM engine (the default, "
+                             "AUTO, runs it with the LDS engine: the comparison)",
     "rs32_1m_recovery": "BASELINE configs[4] as stated: online recovery decode of ONE lost data shard "
                         "(every stripe the same), 1,024 x 1 MiB values, device-resident; D0 led by P0 "
                         "(inverse 1) and D1 led by P1 (inverse 1/245), SURVEY §8d",
@@ -74,7 +74,9 @@ def parse(argv=None):
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
-    ap.add_argument("--engine", default="perm", choices=["perm", "lds"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "perm", "lds"],
+                    help="GF(2^8) engine (cec_set_engine); auto = the library default: LDS for "
+                         "the diff-update, PERM for the other ops")
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
     ap.add_argument("--drain", action="store_true", help="batched parity drain from host diffs")
@@ -91,7 +93,7 @@ def parse(argv=None):
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
     ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_1m_recovery,"
-                                      "rs32_diff_update,rs32_diff_update_lds,rs32_e2e",
+                                      "rs32_diff_update,rs32_diff_update_perm,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -270,11 +272,13 @@ def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES):
     }
 
 
-def load_traffic(workload, ops=("encode", "decode")):
-    """HBM bytes per launch of each op from the committed rocprofv3 --pmc summary
-    (profiles/pmc_traffic.json, written by tools/profile_round.sh)."""
+def load_traffic(workload, ops=("encode", "decode"), engine="perm"):
+    """HBM bytes per launch of each op from the committed rocprofv3 --pmc summary of the
+    engine that ran it (profiles/pmc_traffic.json: PERM, pmc_traffic_lds.json: LDS;
+    written by tools/profile_round.sh)."""
+    name = "pmc_traffic.json" if engine == "perm" else f"pmc_traffic_{engine}.json"
     try:
-        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+        with open(os.path.join(ROOT, "profiles", name)) as f:
             e = json.load(f).get(workload, {})
         return tuple(e.get(f"{op}_hbm_bytes_per_launch") for op in ops)
     except (OSError, ValueError):
@@ -304,6 +308,22 @@ def setup(backend="nccl"):
     if ec.device_check() != ec.CEC_OK:
         raise SystemExit("libcocytus_ec: " + ec.lib().cec_last_error().decode())
     return torch, dist, ec, world, rank
+
+
+ENGINES = {"auto": 2, "perm": 0, "lds": 1}  # cec_engine
+
+
+def set_engine(ec, name):
+    ec.set_engine(ENGINES[name])
+
+
+def engine_of(ec, diff_update):
+    """The engine an op runs with under the current setting (AUTO: LDS for the
+    diff-update, PERM for the others; cocytus_ec.h)."""
+    e = ec.get_engine()
+    if e == ec.CEC_ENGINE_AUTO:
+        return "lds" if diff_update else "perm"
+    return "lds" if e == ec.CEC_ENGINE_LDS else "perm"
 
 
 def share_layout(stripes, lo, hi):
@@ -433,7 +453,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
             "unit": "GB/s",
             "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
             "traffic": enc_traffic,
-            "kernel": f"combine_kernel<{k},{m},{'PermEngine' if args.engine == 'perm' else 'LdsEngine'},"
+            "kernel": f"combine_kernel<{k},{m},{'LdsEngine' if engine_of(ec, False) == 'lds' else 'PermEngine'},"
                       "kAccNone,exact> (cec_encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
             "launch_ms": round(enc_ms, 4),
@@ -529,7 +549,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         dist.barrier()
     du_t = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
     ms = sum(du_t) / args.steps
-    lds = ec.get_engine() == ec.CEC_ENGINE_LDS
+    lds = engine_of(ec, True) == "lds"
     chk = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
     ec.encode_region(k, m, mat, data, chk, T, stream)
     torch.cuda.synchronize()
@@ -548,9 +568,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
                      "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(du_t), 4),
                      "kernel": f"combine_kernel<2,3,{'LdsEngine' if lds else 'PermEngine'},kAccAllButLast,exact> "
                                "(cec_diff_update, install)",
-                     # (profiles/pmc_traffic.json holds the default engine's passes; the LDS
-                     # engine's are in profiles/r03s2_lds_summary.md)
-                     "traffic": None if lds else load_traffic("rs32_diff_update", ("diff_update",))[0]},
+                     "traffic": load_traffic("rs32_diff_update", ("diff_update",), "lds" if lds else "perm")[0]},
         "engine": "lds" if lds else "perm",
         "verified": bool(ok and bad == 0.0),
     }
@@ -736,7 +754,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
 def run_device(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
 
-    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+    set_engine(ec, args.engine)
     r = measure_device(torch, dist, ec, world, rank, args.workload, args)
     strong = None
     if not args.no_strong:
@@ -748,13 +766,13 @@ def run_device(args):
     also = {}
     for w in [x for x in args.also.split(",") if x and x != args.workload]:
         torch.cuda.empty_cache()
-        if w in ("rs32_diff_update", "rs32_diff_update_lds"):
-            if w == "rs32_diff_update_lds":
-                ec.set_engine(ec.CEC_ENGINE_LDS)
+        if w in ("rs32_diff_update", "rs32_diff_update_perm"):
+            if w == "rs32_diff_update_perm":
+                ec.set_engine(ec.CEC_ENGINE_PERM)
             try:
                 also[w] = measure_diff_update(torch, dist, ec, world, rank, args)
             finally:
-                ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+                set_engine(ec, args.engine)
             continue
         if w == "rs32_e2e":
             also[w] = measure_e2e(torch, dist, ec, world, rank, args)
@@ -762,14 +780,14 @@ def run_device(args):
         if w == "rs32_1m_recovery":
             also[w] = measure_recovery_decode(torch, dist, ec, world, rank, args)
             continue
-        engine = args.engine
+        engine = engine_of(ec, False)
         if w == "rs32_4k_lds":
             ec.set_engine(ec.CEC_ENGINE_LDS)
             engine = "lds"
         try:
             o = measure_device(torch, dist, ec, world, rank, "rs32_4k" if w == "rs32_4k_lds" else w, args)
         finally:
-            ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+            set_engine(ec, args.engine)
         also[w] = {
             "value": round(o["value"], 2), "unit": "GiB/s",
             "ms_per_step": round(o["ms_per_step"], 4),
@@ -804,7 +822,8 @@ def run_device(args):
                 "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
                 "bytes_per_shard_per_gpu": r["bytes_total"],
                 "parallelism": f"{world} x independent stripe batches, no collective",
-                "engine": args.engine,
+                "engine": args.engine if args.engine != "auto" else "auto (PERM for encode / decode, "
+                                                                     "LDS for the diff-update)",
             },
             "roofline": r["roofline"],
             "decode_roofline": r["decode_roofline"],
@@ -1002,7 +1021,7 @@ def run_ops(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
     from oracle import pyoracle
 
-    ec.set_engine(ec.CEC_ENGINE_LDS if args.engine == "lds" else ec.CEC_ENGINE_PERM)
+    set_engine(ec, args.engine)
     k, m, n, B = 3, 2, 4096, 65536
     T = n * B
     mat = ec.coding_matrix(k, m)

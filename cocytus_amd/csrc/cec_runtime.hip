@@ -71,7 +71,15 @@ struct DevInfo {
     char msg[256] = "";
 };
 static DevInfo g_dev[64];
-static std::atomic<int> g_engine{CEC_ENGINE_PERM};
+static std::atomic<int> g_engine{CEC_ENGINE_AUTO};
+
+// The engine an op runs with, read once per op (its tables and its kernel must agree):
+// the process-wide setting, or under AUTO the one measured faster for the op --
+// `lds_op` for the fused diff-update, PERM for the others (cocytus_ec.h).
+static int op_engine(bool lds_op) {
+    const int e = g_engine.load();
+    return e == CEC_ENGINE_AUTO ? (lds_op ? CEC_ENGINE_LDS : CEC_ENGINE_PERM) : e;
+}
 
 static int current_device(int *dev) {
     int n = 0;
@@ -609,12 +617,13 @@ static void build_patterns(const std::vector<Combo> &combos, size_t g, int engin
 
 // `used`: which combos the launch's tiles name (NULL = all; a persistent pattern table
 // may hold more than one launch uses: the kernel shape is chosen from the used ones).
+// `lds_op`: the op AUTO runs with the LDS engine (op_engine).
 static int run_combos(int dev, const Streams &st, const std::vector<Combo> &combos,
                       const cec_plan *plan, uint64_t implicit_len, hipStream_t stream,
-                      const std::vector<char> *used = nullptr) {
+                      const std::vector<char> *used = nullptr, bool lds_op = false) {
     size_t max_out = 0;
     for (const Combo &c : combos) max_out = std::max(max_out, c.outs.size());
-    const int engine = g_engine.load();
+    const int engine = op_engine(lds_op);
     const size_t groups = (max_out + kPatL - 1) / kPatL;
     for (size_t g = 0; g < groups; ++g) {
         std::vector<Pattern> pats;
@@ -674,7 +683,8 @@ CEC_API int cec_device_check(void) {
     return current_device(&dev);
 }
 CEC_API int cec_set_engine(cec_engine e) {
-    if (e != CEC_ENGINE_PERM && e != CEC_ENGINE_LDS) return fail(CEC_EINVAL, "bad engine %d", e);
+    if (e != CEC_ENGINE_PERM && e != CEC_ENGINE_LDS && e != CEC_ENGINE_AUTO)
+        return fail(CEC_EINVAL, "bad engine %d", e);
     g_engine.store(e);
     return CEC_OK;
 }
@@ -713,7 +723,7 @@ static int region_launch(int dev, const void *src, int multby, size_t n, void *d
                          bool plain, uint32_t flags = 0, bool *released = nullptr) {
     const uint64_t n_tiles = (n + kTile - 1) / kTile;
     if (n_tiles > 0xFFFFFFFFull) return fail(CEC_EINVAL, "region too large");
-    const int engine = g_engine.load();
+    const int engine = op_engine(false);
     const int key = (engine << 9) | (add ? 256 : 0) | multby;
     const bool capturing = !plain && stream_capturing(s);
     RegionMemo &m = t_region;
@@ -859,7 +869,7 @@ CEC_API int cec_diff_update(int k, int m, const int *matrix, uint8_t *const *dat
             c.outs.push_back(o);
         }
     }
-    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr, true);
 }
 
 CEC_API int cec_set_diff(int k, const uint8_t *const *data, const uint8_t *staging, uint8_t *diff,

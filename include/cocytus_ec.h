@@ -81,18 +81,20 @@ typedef struct cec_extent {
  * walk (load balance across mixed 256 B .. 1 MiB values).  Build once per batch. */
 typedef struct cec_plan cec_plan;
 
-/* GF(2^8) engine used by the kernels.  Both are bit-exact and within 1-2 % of each
- * other.  PERM (default) looks up three 8-entry byte tables per coefficient with
- * v_perm_b32 (pure VALU, no LDS); LDS stages one 256-entry product row per
- * coefficient, exp[log x + log c] built from the log / antilog tables, in LDS (one
- * ds_read_u8 per byte). */
-typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1 } cec_engine;
+/* GF(2^8) engine used by the kernels.  Both are bit-exact and within a few % of each
+ * other.  PERM looks up three 8-entry byte tables per coefficient with v_perm_b32
+ * (pure VALU, no LDS); LDS stages one 256-entry product row per coefficient,
+ * exp[log x + log c] built from the log / antilog tables, in LDS (one ds_read_u8 per
+ * byte).  AUTO (default) picks per op the engine measured faster for it: LDS for the
+ * fused diff-update (cec_diff_update, 1.4-3.0 % ahead on three boxes), PERM for every
+ * other op. */
+typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1, CEC_ENGINE_AUTO = 2 } cec_engine;
 
 /* ---- runtime ---- */
 const char *cec_version(void);
 const char *cec_last_error(void);               /* thread-local message of the last failure */
 int cec_device_check(void);                     /* CEC_OK if the current device is gfx950 */
-int cec_set_engine(cec_engine e);               /* process-wide; default CEC_ENGINE_PERM */
+int cec_set_engine(cec_engine e);               /* process-wide; default CEC_ENGINE_AUTO */
 cec_engine cec_get_engine(void);
 /* Occupancy of the streaming kernels: at most waves_per_cu waves of one launch per CU
  * (0 = as many as fit).  Process-wide; the initial value comes from the

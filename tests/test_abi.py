@@ -148,11 +148,17 @@ def test_arena_stride_is_odd_pages(lib):
         assert s >= n and s % 4096 == 0 and (s // 4096) % 2 == 1 and s - n < 2 * 4096
 
 
-def test_default_engine_is_perm(lib):
-    """The product default is the PERM engine (1-2 % ahead of the LDS engine in bench
-    processes); LDS stays selectable and both are in every GPU parity
-    test."""
-    assert lib.get_engine() == lib.CEC_ENGINE_PERM
+def test_default_engine_is_auto(lib):
+    """The product default is AUTO: per op the engine measured faster for it, LDS for the
+    fused diff-update, PERM for the others.  PERM and LDS stay selectable
+    and both are in every GPU parity test; AUTO is what every test that leaves the engine
+    alone runs."""
+    assert lib.get_engine() == lib.CEC_ENGINE_AUTO
+    for e in (lib.CEC_ENGINE_PERM, lib.CEC_ENGINE_LDS, lib.CEC_ENGINE_AUTO):
+        lib.set_engine(e)
+        assert lib.get_engine() == e
+    with pytest.raises(lib.CecError):
+        lib.set_engine(3)
 
 
 def test_waves_per_cu_knob(lib):

@@ -205,10 +205,10 @@ def test_bench_arguments():
     import bench
 
     a = bench.parse([])
-    assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "perm")
+    assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "auto")
     assert 1 <= a.steps <= 100 and a.warmup >= 1
     assert set(a.also.split(",")) == {"rs32_4k_lds", "rs32_mixed", "rs32_1m", "rs42_64k",
-                                      "rs32_1m_recovery", "rs32_diff_update", "rs32_diff_update_lds",
+                                      "rs32_1m_recovery", "rs32_diff_update", "rs32_diff_update_perm",
                                       "rs32_e2e"}
     assert not a.no_strong
     assert bench.parse(["--also="]).also == ""

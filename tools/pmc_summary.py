@@ -113,9 +113,10 @@ def main(out, rnd, engine="perm"):
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    if engine == "perm":  # bench.py's `traffic` is the default (PERM) engine's
-        with open(os.path.join(prof, "pmc_traffic.json"), "w") as f:
-            json.dump(traffic, f, indent=1)
+    # bench.py's `traffic` per engine: pmc_traffic.json (PERM), pmc_traffic_lds.json
+    with open(os.path.join(prof, "pmc_traffic.json" if engine == "perm" else f"pmc_traffic_{engine}.json"),
+              "w") as f:
+        json.dump(traffic, f, indent=1)
     md = [f"# rocprofv3 summary ({rnd}, engine {engine})", "",
           f"bench.py --steps 10 --warmup 2 --no-strong --engine {engine} per workload "
           "(rs32_diff_update: --also=rs32_diff_update, only its",

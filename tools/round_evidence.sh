@@ -21,7 +21,7 @@ $B --e2e                               > "$OUT/bench_e2e.jsonl"     2> "$OUT/ben
 $B --e2e --e2e-zero-copy               > "$OUT/bench_e2e_zc.jsonl"  2> "$OUT/bench_e2e_zc.err"
 $B --drain --steps 5 --warmup 2        > "$OUT/bench_drain.jsonl"   2> "$OUT/bench_drain.err"
 $B --recovery --steps 5                > "$OUT/bench_recovery.jsonl" 2> "$OUT/bench_recovery.err"
-$B --ops                               > "$OUT/bench_ops.jsonl"     2> "$OUT/bench_ops.err"
+$B --ops --engine perm                 > "$OUT/bench_ops.jsonl"     2> "$OUT/bench_ops.err"
 $B --ops --engine lds                  > "$OUT/bench_ops_lds.jsonl" 2> "$OUT/bench_ops_lds.err"
 timeout -k 10 200 tools/hbm_mix.bin arena random 64  > "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/hbm_mix.bin arena random 256 >> "$OUT/hbm_mix.txt" 2>&1
