@@ -317,12 +317,12 @@ def set_engine(ec, name):
     ec.set_engine(ENGINES[name])
 
 
-def engine_of(ec, diff_update):
+def engine_of(ec, lds_op):
     """The engine an op runs with under the current setting (AUTO: LDS for the
-    diff-update, PERM for the others; cocytus_ec.h)."""
+    diff-update and the single-mask decode, `lds_op`; PERM for the others; cocytus_ec.h)."""
     e = ec.get_engine()
     if e == ec.CEC_ENGINE_AUTO:
-        return "lds" if diff_update else "perm"
+        return "lds" if lds_op else "perm"
     return "lds" if e == ec.CEC_ENGINE_LDS else "perm"
 
 
@@ -626,7 +626,7 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
         }
     plan.destroy()
     del ar, data, parity, out
-    return {"workload": EXTRA_WORKLOADS["rs32_1m_recovery"], "cases": cases,
+    return {"workload": EXTRA_WORKLOADS["rs32_1m_recovery"], "cases": cases, "engine": engine_of(ec, True),
             "value": min(c["value"] for c in cases.values()), "unit": "GiB/s rebuilt (slower case)",
             "decode_frac": min(c["decode_frac"] for c in cases.values()),
             "verified": all(c["verified"] for c in cases.values())}
@@ -822,8 +822,9 @@ def run_device(args):
                 "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
                 "bytes_per_shard_per_gpu": r["bytes_total"],
                 "parallelism": f"{world} x independent stripe batches, no collective",
-                "engine": args.engine if args.engine != "auto" else "auto (PERM for encode / decode, "
-                                                                     "LDS for the diff-update)",
+                "engine": args.engine if args.engine != "auto" else "auto (PERM for the encode and the "
+                                                                     "rotating decode, LDS for the diff-update "
+                                                                     "and single-mask decodes)",
             },
             "roofline": r["roofline"],
             "decode_roofline": r["decode_roofline"],

@@ -75,7 +75,8 @@ static std::atomic<int> g_engine{CEC_ENGINE_AUTO};
 
 // The engine an op runs with, read once per op (its tables and its kernel must agree):
 // the process-wide setting, or under AUTO the one measured faster for the op --
-// `lds_op` for the fused diff-update, PERM for the others (cocytus_ec.h).
+// `lds_op` for the fused diff-update and the single-mask decode, PERM for the others
+// (cocytus_ec.h).
 static int op_engine(bool lds_op) {
     const int e = g_engine.load();
     return e == CEC_ENGINE_AUTO ? (lds_op ? CEC_ENGINE_LDS : CEC_ENGINE_PERM) : e;
@@ -1069,7 +1070,10 @@ CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, i
             c.outs.push_back(o);
         }
     }
-    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
+    // AUTO: one recovery mask for the whole batch (a server rebuilding one lid) runs the
+    // LDS engine (2-5 % ahead of PERM, profiles/r03_evidence/engine_auto/), erasures that
+    // vary per value run PERM (ahead by 2-3 % on the bench's rotating masks)
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr, n_masks == 1);
 }
 
 CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected) {

@@ -250,5 +250,21 @@ engprev)
   # the negative control of case eng alone (tools/ab_prev uploaded for this call)
   timeout -k 10 300 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u -m pytest tests/test_gpu_runtime.py -x -q --timeout 240 --timeout-method thread -k "engine_switch" > gpurun_out/r03engprev/pytest_eng_prev.log 2>&1; echo "prev rc=$?"
   ;;
+fixdec)
+  # round-3 (second session): engine per op for the fixed-mask decode (one recovery mask for
+  # the whole batch: configs[4], --ops' decode) -- PERM vs LDS, interleaved, three rounds
+  for i in 1 2 3; do
+    run rec_perm_$i 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine perm
+    run rec_lds_$i 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine lds
+    run ops_perm_$i 200 python -u bench.py --ops --engine perm
+    run ops_lds_$i 200 python -u bench.py --ops --engine lds
+  done
+  ;;
+delay)
+  # round-3 (second session): what the LDS engine adds between a wave's loads and stores,
+  # on bare XOR streams (the fixed-mask decode ran 5 % faster with two staged rows)
+  timeout -k 10 200 tools/delay_probe.bin 1024 > gpurun_out/r03delay/delay_1g.jsonl 2>&1 && \
+  timeout -k 10 200 tools/delay_probe.bin 256 > gpurun_out/r03delay/delay_256m.jsonl 2>&1
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
