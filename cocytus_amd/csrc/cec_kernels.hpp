@@ -286,7 +286,7 @@ enum : int { kAccNone = 0, kAccAll = 1, kAccAllButLast = 2, kAccRuntime = 3 };
 // template parameter, so the batched kernels carry no epilogue at all).
 // LDS engine, full aligned tiles: stage the product rows before the stream loads (the
 // fast path in combine_kernel) for the diff-update shapes only (2 inputs, parity
-// read-modify-write).  There it ran the diff-update + install 3.5 % faster; in the
+// read-modify-write).  There it ran the diff-update + install 2.4 % faster; in the
 // encode (3 x 2) the second path's registers cost SGPR spills and occupancy (+10 %),
 // and the fixed-mask decode / residual (3 x 1) lost 2-3 %
 // (profiles/r03_evidence/lds_early_rows/).

@@ -463,8 +463,9 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 // (n_pats patterns, then the LDS engine's rows) already on the device.  The caller
 // checks hipGetLastError.
 // *released: whether every wave of the launch ends with a system-scope release
-// (kFlagSysRelease asked for, and honoured: only the narrow 1 x 1 launches carry it).  hpats / used: the host copies of the launch's patterns and
-// which of them its tiles name (NULL: all), for the stream check below.
+// (kFlagSysRelease asked for, and honoured: only the narrow 1 x 1 launches carry it).
+// hpats / used: the host copies of the launch's patterns and which of them its tiles
+// name (NULL: all), for the stream check below.
 enum KernelKind { kKindNarrow, kKindExact, kKindGeneric };
 
 // Every stream a kernel of `kind` will dereference for each used pattern, read from the
