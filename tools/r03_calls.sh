@@ -266,5 +266,25 @@ delay)
   timeout -k 10 200 tools/delay_probe.bin 1024 > gpurun_out/r03delay/delay_1g.jsonl 2>&1 && \
   timeout -k 10 200 tools/delay_probe.bin 256 > gpurun_out/r03delay/delay_256m.jsonl 2>&1
   ;;
+occ)
+  # round-3 (second session): is the LDS engine's fixed-mask decode lead an occupancy
+  # effect (76 VGPRs: 6 waves / SIMD against PERM's 8)?  PERM with the occupancy cap
+  # (CEC_WAVES_PER_CU = waves per CU) against LDS uncapped, configs[4] decode + --ops
+  for i in 1 2; do
+    for w in 0 16 24 28; do
+      run rec_perm_w${w}_$i 200 env CEC_WAVES_PER_CU=$w python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine perm
+    done
+    run rec_lds_$i 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine lds
+  done
+  ;;
+occ2)
+  # round-3 (second session): occupancy cap per op -- the diff-update (PERM and LDS) and the
+  # metric's rotating decode at 16 / 20 / 24 / 28 waves per CU against uncapped
+  for i in 1 2; do
+    for w in 0 16 20 24 28; do
+      run du_w${w}_$i 200 env CEC_WAVES_PER_CU=$w python -u bench.py --also=rs32_diff_update,rs32_diff_update_perm --no-cpu-baseline --no-strong
+    done
+  done
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
