@@ -286,5 +286,12 @@ occ2)
     done
   done
   ;;
+gloo)
+  # round-3 (second session): the default line with every workload at 2 ranks and the new
+  # ones at 8 ranks, all on this one card (gloo): the driver's multi-GPU path end to end
+  CEC_BENCH_DEVICE=0 timeout -k 10 400 python -u bench.py --gpus 2 > gpurun_out/r03gloo/gloo2.jsonl 2> gpurun_out/r03gloo/gloo2.err && \
+  CEC_BENCH_WATCHDOG=60 CEC_BENCH_DEVICE=0 timeout -k 10 500 python -u bench.py --gpus 8 --also=rs32_1m_recovery,rs32_diff_update,rs32_diff_update_perm \
+      > gpurun_out/r03gloo/gloo8.jsonl 2> gpurun_out/r03gloo/gloo8.err
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
