@@ -293,5 +293,15 @@ gloo)
   CEC_BENCH_WATCHDOG=60 CEC_BENCH_DEVICE=0 timeout -k 10 500 python -u bench.py --gpus 8 --also=rs32_1m_recovery,rs32_diff_update,rs32_diff_update_perm \
       > gpurun_out/r03gloo/gloo8.jsonl 2> gpurun_out/r03gloo/gloo8.err
   ;;
+profrec)
+  # round-3 (second session): rocprofv3 for the configs[4] recovery decode under AUTO (the
+  # LDS engine's 3 x 1 kernel; the metric's kernels in the same process are PERM)
+  O=$GRAFT_REPO_ROOT/gpurun_out/r03profrec; R=$GRAFT_REPO_ROOT
+  cd /tmp && export TMPDIR=/tmp
+  A="--steps 10 --warmup 2 --no-cpu-baseline --no-strong --also=rs32_1m_recovery"
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py $A > $O/trace.log 2>&1 && \
+  timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 $R/bench.py $A > $O/fetch.log 2>&1 && \
+  timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 $R/bench.py $A > $O/write.log 2>&1
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
