@@ -303,5 +303,15 @@ profrec)
   timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- python3 $R/bench.py $A > $O/fetch.log 2>&1 && \
   timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- python3 $R/bench.py $A > $O/write.log 2>&1
   ;;
+engw|engw2|engw3)
+  # round-3 (second session): PERM vs LDS on the other device-resident workloads (encode +
+  # rotating decode), interleaved, two rounds
+  for i in 1 2; do
+    for w in rs32_1m rs42_64k rs32_mixed; do
+      run ${w}_perm_$i 200 python -u bench.py --workload $w --also= --no-cpu-baseline --no-strong --engine perm
+      run ${w}_lds_$i 200 python -u bench.py --workload $w --also= --no-cpu-baseline --no-strong --engine lds
+    done
+  done
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
