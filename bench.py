@@ -436,9 +436,11 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     dec_bytes = (k + 1) * bytes_total  # per decode launch (read K survivors, write 1)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    enc_traffic, dec_traffic = load_traffic(workload)
+    # the engine both ops ran with (AUTO: LDS for values of 64 KiB and more, cocytus_ec.h)
+    eng = engine_of(ec, bytes_total >= (64 << 10) * max(1, B))
+    enc_traffic, dec_traffic = load_traffic(workload, engine=eng)
     return {
-        "k": k, "m": m, "n": n, "B": B, "what": what, "bytes_total": bytes_total,
+        "k": k, "m": m, "n": n, "B": B, "what": what, "bytes_total": bytes_total, "engine": eng,
         "value": payload / elapsed / 2**30,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "verified": ok and bad == 0.0,
@@ -453,7 +455,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
             "unit": "GB/s",
             "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
             "traffic": enc_traffic,
-            "kernel": f"combine_kernel<{k},{m},{'LdsEngine' if engine_of(ec, False) == 'lds' else 'PermEngine'},"
+            "kernel": f"combine_kernel<{k},{m},{'LdsEngine' if eng == 'lds' else 'PermEngine'},"
                       "kAccNone,exact> (cec_encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
             "launch_ms": round(enc_ms, 4),
@@ -780,10 +782,8 @@ def run_device(args):
         if w == "rs32_1m_recovery":
             also[w] = measure_recovery_decode(torch, dist, ec, world, rank, args)
             continue
-        engine = engine_of(ec, False)
         if w == "rs32_4k_lds":
             ec.set_engine(ec.CEC_ENGINE_LDS)
-            engine = "lds"
         try:
             o = measure_device(torch, dist, ec, world, rank, "rs32_4k" if w == "rs32_4k_lds" else w, args)
         finally:
@@ -794,13 +794,13 @@ def run_device(args):
             "workload": f"RS({o['k']},{o['m']}) encode + single-shard decode, "
                         f"{'%d B' % o['n'] if o['n'] else 'mixed 256 B-1 MiB'} values, "
                         f"{o['B']} stripes per GPU ({o['what']})",
-            "engine": engine,
+            "engine": o["engine"],
             "encode_frac": o["roofline"]["frac"], "decode_frac": o["decode_roofline"]["frac"],
             "encode_ms": o["roofline"]["launch_ms"], "decode_ms": o["decode_roofline"]["launch_ms"],
             "verified": o["verified"],
         }
         if w == "rs32_4k_lds":
-            also[w]["kernel"] = o["roofline"]["kernel"].replace("PermEngine", "LdsEngine")
+            also[w]["kernel"] = o["roofline"]["kernel"]
     if rank == 0:
         k, m, n, B = r["k"], r["m"], r["n"], r["B"]
         res = {
@@ -822,9 +822,9 @@ def run_device(args):
                 "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
                 "bytes_per_shard_per_gpu": r["bytes_total"],
                 "parallelism": f"{world} x independent stripe batches, no collective",
-                "engine": args.engine if args.engine != "auto" else "auto (PERM for the encode and the "
-                                                                     "rotating decode, LDS for the diff-update "
-                                                                     "and single-mask decodes)",
+                "engine": args.engine if args.engine != "auto" else
+                          f"auto ({r['engine'].upper()} for this workload's encode and decode; LDS for the "
+                          "diff-update, single-mask decodes and values of 64 KiB and more)",
             },
             "roofline": r["roofline"],
             "decode_roofline": r["decode_roofline"],

@@ -784,6 +784,15 @@ CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void
     return region_launch(dev, src, multby, nbytes, dst, add, static_cast<hipStream_t>(stream), false);
 }
 
+// AUTO's value-size rule for the encode and the decode: values of 64 KiB and more (and
+// contiguous regions) run the LDS engine, smaller ones PERM.  Measured on two boxes, two
+// rounds each (profiles/r03_evidence/engine_auto/workloads_box*/): at 64 KiB, 1 MiB and
+// the mixed 256 B - 1 MiB batch the LDS engine led the encode by 0-1.6 % and the rotating
+// decode by 2.8-3.7 %; at 4 KiB the encode ties and PERM leads the rotating decode by 2-3 %.
+static bool large_values(const cec_plan *plan) {
+    return !plan || plan->total >= (uint64_t(64) << 10) * static_cast<uint64_t>(std::max(plan->n_ext, 1));
+}
+
 static int encode_common(int k, int m, const int *matrix, const uint8_t *const *data,
                          uint8_t *const *parity, const cec_plan *plan, uint64_t len,
                          void *stream) {
@@ -808,7 +817,7 @@ static int encode_common(int k, int m, const int *matrix, const uint8_t *const *
         for (int j = 0; j < k; ++j) o.coef[j] = MATRIX(k + p, j);
         c.outs.push_back(o);
     }
-    return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream));
+    return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream), nullptr, large_values(plan));
 }
 
 // Ops with one pattern index every tile's pattern field into a one-entry table: it must be 0.
@@ -1072,9 +1081,11 @@ CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, i
         }
     }
     // AUTO: one recovery mask for the whole batch (a server rebuilding one lid) runs the
-    // LDS engine (2-5 % ahead of PERM, profiles/r03_evidence/engine_auto/), erasures that
-    // vary per value run PERM (ahead by 2-3 % on the bench's rotating masks)
-    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr, n_masks == 1);
+    // LDS engine (2-5 % ahead of PERM, profiles/r03_evidence/engine_auto/), and so do
+    // large values (large_values); erasures that vary per 4 KiB value run PERM (ahead by
+    // 2-3 % on the bench's rotating masks)
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr,
+                      n_masks == 1 || large_values(plan));
 }
 
 CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected) {

@@ -85,10 +85,11 @@ typedef struct cec_plan cec_plan;
  * other.  PERM looks up three 8-entry byte tables per coefficient with v_perm_b32
  * (pure VALU, no LDS); LDS stages one 256-entry product row per coefficient,
  * exp[log x + log c] built from the log / antilog tables, in LDS (one ds_read_u8 per
- * byte).  AUTO (default) picks per op the engine measured faster for it: LDS for the
- * fused diff-update (cec_diff_update, 1.4-3.0 % ahead on four boxes) and for a decode
- * with one mask for the whole batch (cec_decode, n_masks == 1: 2-5 % ahead), PERM for
- * every other op, including decodes whose erasures vary per value. */
+ * byte).  AUTO (default) picks per op the engine measured faster for it:
+ * LDS for the fused diff-update (cec_diff_update), for a decode with one mask for the
+ * whole batch (cec_decode, n_masks == 1), and for encodes and decodes of values of
+ * 64 KiB and more (a plan's mean extent; cec_encode_region always); PERM for every
+ * other op, including encodes and per-value rotating decodes of smaller values. */
 typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1, CEC_ENGINE_AUTO = 2 } cec_engine;
 
 /* ---- runtime ---- */

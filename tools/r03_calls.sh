@@ -307,7 +307,7 @@ engw|engw2|engw3)
   # round-3 (second session): PERM vs LDS on the other device-resident workloads (encode +
   # rotating decode), interleaved, two rounds
   for i in 1 2; do
-    for w in rs32_1m rs42_64k rs32_mixed; do
+    for w in rs32_4k rs32_1m rs42_64k rs32_mixed; do
       run ${w}_perm_$i 200 python -u bench.py --workload $w --also= --no-cpu-baseline --no-strong --engine perm
       run ${w}_lds_$i 200 python -u bench.py --workload $w --also= --no-cpu-baseline --no-strong --engine lds
     done
