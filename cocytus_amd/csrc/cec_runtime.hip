@@ -786,7 +786,7 @@ CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void
 
 // AUTO's value-size rule for the encode and the decode: values of 64 KiB and more (and
 // contiguous regions) run the LDS engine, smaller ones PERM.  Measured on two boxes, two
-// rounds each (profiles/r03_evidence/engine_auto/workloads_box*/): at 64 KiB, 1 MiB and
+// rounds each (profiles/r03_evidence/engine_auto/workloads_box*/; a third box agreed): at 64 KiB, 1 MiB and
 // the mixed 256 B - 1 MiB batch the LDS engine led the encode by 0-1.6 % and the rotating
 // decode by 2.8-3.7 %; at 4 KiB the encode ties and PERM leads the rotating decode by 2-3 %.
 static bool large_values(const cec_plan *plan) {

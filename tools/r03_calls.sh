@@ -226,7 +226,7 @@ rec)
   run rec2 200 python -u bench.py --also=rs32_1m_recovery --no-cpu-baseline --no-strong --engine lds
   run pytest2 400 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 300 --timeout-method thread -k "two_ranks"
   ;;
-q2|q3|q4|q5)
+q2|q3|q4|q5|q6|q7)
   # round-3 (second session) final check on the final tree, as the driver runs it
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03$call/pytest.log 2>&1 && \
   timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03$call/smoke.log 2>&1 && \
