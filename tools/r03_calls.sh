@@ -313,5 +313,10 @@ engw|engw2|engw3)
     done
   done
   ;;
+proflds)
+  # round-3 (second session): rocprofv3 for the LDS engine on the larger-value workloads
+  # (what AUTO runs there): kernel trace + FETCH / WRITE passes
+  PROF_ENGINE=lds PROF_WORKLOADS="rs32_1m rs42_64k rs32_mixed" bash tools/profile_round.sh r03s2_lds_large || exit $?
+  ;;
 *) echo "usage: bash tools/r03_calls.sh <b|c|e|...|r>" >&2; exit 2 ;;
 esac
