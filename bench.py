@@ -75,8 +75,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
     ap.add_argument("--engine", default="auto", choices=["auto", "perm", "lds"],
-                    help="GF(2^8) engine (cec_set_engine); auto = the library default: LDS for "
-                         "the diff-update, PERM for the other ops")
+                    help="GF(2^8) engine (cec_set_engine); auto = the library default: per op, "
+                         "LDS for the diff-update, single-mask decodes and values of 64 KiB and "
+                         "more, PERM for the rest (cocytus_ec.h)")
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
     ap.add_argument("--drain", action="store_true", help="batched parity drain from host diffs")
@@ -318,8 +319,9 @@ def set_engine(ec, name):
 
 
 def engine_of(ec, lds_op):
-    """The engine an op runs with under the current setting (AUTO: LDS for the
-    diff-update and the single-mask decode, `lds_op`; PERM for the others; cocytus_ec.h)."""
+    """The engine an op runs with under the current setting.  `lds_op`: whether AUTO runs
+    this op with the LDS engine (the diff-update, single-mask decodes, values of 64 KiB
+    and more; cocytus_ec.h), which the caller decides from the op and its values."""
     e = ec.get_engine()
     if e == ec.CEC_ENGINE_AUTO:
         return "lds" if lds_op else "perm"
