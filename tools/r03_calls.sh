@@ -204,11 +204,11 @@ z)
   run ops_new 200 python -u bench.py --ops --engine lds
   run ops_prev 200 env CEC_LIB_PATH=tools/ab_prev/libcocytus_ec.so python -u bench.py --ops --engine lds
   ;;
-final2)
+final2|final3)
   # round-3 (second session) evidence on the final build: GPU suite, then every DESIGN §5
   # number (no profiles; those are call final2p)
-  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03final2/pytest.log 2>&1 && \
-  EVID_NO_PROF=1 bash tools/round_evidence.sh r03s2
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > gpurun_out/r03$call/pytest.log 2>&1 && \
+  EVID_NO_PROF=1 bash tools/round_evidence.sh r03$call
   ;;
 final2p)
   # round-3 (second session) rocprofv3 on the final build: kernel trace + FETCH / WRITE passes
