@@ -215,10 +215,10 @@ final2p)
   bash tools/profile_round.sh r03s2 || exit $?
   PROF_ENGINE=lds PROF_WORKLOADS="rs32_4k rs32_diff_update" bash tools/profile_round.sh r03s2_lds || exit $?
   ;;
-san2)
+san2|san3)
   # round-3 (second session) sanitizer reruns on the final host code (cec_last_sync)
-  timeout -k 10 600 bash tools/asan.sh run > gpurun_out/r03san2/asan.txt 2>&1 && \
-  timeout -k 10 600 bash tools/tsan.sh run > gpurun_out/r03san2/tsan.txt 2>&1
+  timeout -k 10 600 bash tools/asan.sh run > gpurun_out/r03$call/asan.txt 2>&1 && \
+  timeout -k 10 600 bash tools/tsan.sh run > gpurun_out/r03$call/tsan.txt 2>&1
   ;;
 rec)
   # round-3 (second session): configs[4] as stated (fixed-mask recovery decode, 1 MiB values)
