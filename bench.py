@@ -60,8 +60,8 @@ EXTRA_WORKLOADS = {
                 "(H2D -> kernels -> D2H pipelined over HIP streams)",
     "rs32_4k_lds": "the metric's workload with the LDS engine: GF(2^8) products from 256-entry "
                    "log/antilog product rows staged in LDS (the north star's named kernel form)",
-    "rs32_diff_update_perm": "the per-SET diff-update + install with the PERM engine (the default, "
-                             "AUTO, runs it with the LDS engine: the comparison)",
+    "rs32_diff_update_lds": "the per-SET diff-update + install with the LDS engine (AUTO runs it with "
+                            "PERM: the comparison, DESIGN.md §4)",
     "rs32_1m_recovery": "BASELINE configs[4] as stated: online recovery decode of ONE lost data shard "
                         "(every stripe the same), 1,024 x 1 MiB values, device-resident; D0 led by P0 "
                         "(inverse 1) and D1 led by P1 (inverse 1/245), SURVEY §8d",
@@ -75,9 +75,9 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
     ap.add_argument("--engine", default="auto", choices=["auto", "perm", "lds"],
-                    help="GF(2^8) engine (cec_set_engine); auto = the library default: per op, "
-                         "LDS for the diff-update, single-mask decodes and values of 64 KiB and "
-                         "more, PERM for the rest (cocytus_ec.h)")
+                    help="GF(2^8) engine (cec_set_engine); auto = the library default: LDS for "
+                         "single-mask decodes and decodes of values of 64 KiB and more, PERM for "
+                         "every other op (cocytus_ec.h)")
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
     ap.add_argument("--drain", action="store_true", help="batched parity drain from host diffs")
@@ -94,7 +94,7 @@ def parse(argv=None):
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
     ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_1m_recovery,"
-                                      "rs32_diff_update,rs32_diff_update_perm,rs32_e2e",
+                                      "rs32_diff_update,rs32_diff_update_lds,rs32_e2e",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -273,17 +273,73 @@ def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES):
     }
 
 
-def load_traffic(workload, ops=("encode", "decode"), engine="perm"):
+_CODE_ID = []
+
+
+def this_code_id():
+    """ec.kernel_code_id() of the in-tree library, computed once per process (~2 s)."""
+    if not _CODE_ID:
+        from cocytus_amd import ec
+
+        _CODE_ID.append(ec.kernel_code_id())
+    return _CODE_ID[0]
+
+
+def load_traffic(workload, ops=("encode", "decode"), engine="perm", code_id=None):
     """HBM bytes per launch of each op from the committed rocprofv3 --pmc summary of the
     engine that ran it (profiles/pmc_traffic.json: PERM, pmc_traffic_lds.json: LDS;
-    written by tools/profile_round.sh)."""
+    written by tools/profile_round.sh + tools/pmc_summary.py), and whether it is stale.
+
+    The summary records the device code it measured (`_build.kernel_code_id`: a hash of
+    the library's disassembled gfx950 kernels, ec.kernel_code_id).  When that differs
+    from the library this run loads (`code_id`, default: the in-tree build), or is
+    missing, the bytes describe other kernels: every value is None and stale is True.
+    Returns (values tuple, stale)."""
     name = "pmc_traffic.json" if engine == "perm" else f"pmc_traffic_{engine}.json"
+    none = tuple(None for _ in ops)
     try:
         with open(os.path.join(ROOT, "profiles", name)) as f:
-            e = json.load(f).get(workload, {})
-        return tuple(e.get(f"{op}_hbm_bytes_per_launch") for op in ops)
+            doc = json.load(f)
     except (OSError, ValueError):
-        return tuple(None for _ in ops)
+        return none, True
+    if code_id is None:
+        code_id = this_code_id()
+    if not code_id or doc.get("_build", {}).get("kernel_code_id") != code_id:
+        return none, True
+    e = doc.get(workload, {})
+    return tuple(e.get(f"{op}_hbm_bytes_per_launch") for op in ops), False
+
+
+def device_identity(torch, dev) -> dict:
+    """Which physical GPU this rank ran on: ordinal, name, PCI address and UUID (the
+    N > 1 line must show on its own that N distinct GPUs ran)."""
+    p = torch.cuda.get_device_properties(dev)
+    return {"device": dev, "name": p.name, "arch": p.gcnArchName.split(":")[0],
+            "pci": f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", "uuid": str(p.uuid)}
+
+
+def gather_ranks(dist, mine: dict) -> list:
+    """Every rank's entry, in rank order, on every rank (one all_gather_object, outside
+    every timed region; identity when alone)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [mine]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, mine)
+    return out
+
+
+def ranks_summary(entries: list, backend: str) -> dict:
+    """The N > 1 line's evidence: per rank its device identity and its own
+    step times (before the max over ranks), whether the ranks ran on distinct devices
+    (by UUID and PCI address), and which rank was slowest in each record."""
+    ids = {(e["identity"].get("uuid"), e["identity"].get("pci")) for e in entries}
+    out = {"world_size": len(entries), "backend": backend, "distinct_devices": len(ids) == len(entries),
+           "per_rank": entries}
+    for rec in ("weak", "strong"):
+        ts = [(e[rec]["ms_per_step"], e["rank"]) for e in entries if e.get(rec)]
+        if ts:
+            out[f"slowest_rank_{rec}"] = max(ts)[1]
+    return out
 
 
 def setup(backend="nccl"):
@@ -318,13 +374,12 @@ def set_engine(ec, name):
     ec.set_engine(ENGINES[name])
 
 
-def engine_of(ec, lds_op):
-    """The engine an op runs with under the current setting.  `lds_op`: whether AUTO runs
-    this op with the LDS engine (the diff-update, single-mask decodes, values of 64 KiB
-    and more; cocytus_ec.h), which the caller decides from the op and its values."""
-    e = ec.get_engine()
-    if e == ec.CEC_ENGINE_AUTO:
-        return "lds" if lds_op else "perm"
+def engine_ran(ec):
+    """The engine the calling thread's last op ran with, as the library reports it
+    (cec_last_engine: AUTO resolved per op)."""
+    e = ec.last_engine()
+    if e < 0:
+        raise RuntimeError("cec_last_engine: no op has run on this thread")
     return "lds" if e == ec.CEC_ENGINE_LDS else "perm"
 
 
@@ -379,9 +434,12 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     stream = torch.cuda.current_stream()
     bytes_total = sum(ln for _, ln in stripes)
 
-    for _ in range(args.warmup):
+    eng = {}
+    for _ in range(max(1, args.warmup)):
         ec.encode(k, m, mat, data, parity, enc_plan, stream)
+        eng["encode"] = engine_ran(ec)
         ec.decode(k, m, mat, masks, data + parity, out, dec_plan, stream)
+        eng["decode"] = engine_ran(ec)
     torch.cuda.synchronize()
 
     # One event between consecutive launches: event 2s..2s+1 brackets step s's encode and
@@ -411,6 +469,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     elapsed = pc() - t0  # this rank's K steps; the max over ranks is taken below
     if world > 1:
         dist.barrier()
+    own_elapsed = elapsed
     enc_t = [evs[2 * s].elapsed_ms(evs[2 * s + 1]) for s in range(args.steps)]
     dec_t = [evs[2 * s + 1].elapsed_ms(evs[2 * s + 2]) for s in range(args.steps)]
     enc_ms, dec_ms = sum(enc_t) / args.steps, sum(dec_t) / args.steps  # = rocprof's average
@@ -438,14 +497,17 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     dec_bytes = (k + 1) * bytes_total  # per decode launch (read K survivors, write 1)
     enc_gbps = enc_bytes / (enc_ms * 1e-3) / 1e9
     dec_gbps = dec_bytes / (dec_ms * 1e-3) / 1e9
-    # the engine both ops ran with (AUTO: LDS for values of 64 KiB and more, cocytus_ec.h)
-    eng = engine_of(ec, bytes_total >= (64 << 10) * max(1, B))
-    enc_traffic, dec_traffic = load_traffic(workload, engine=eng)
+    # traffic from the committed PMC summary of the engine each op ran with (the library's
+    # own report, cec_last_engine), if it measured this build's kernels
+    (enc_traffic, _), enc_stale = load_traffic(workload, engine=eng["encode"])
+    (_, dec_traffic), dec_stale = load_traffic(workload, engine=eng["decode"])
     return {
         "k": k, "m": m, "n": n, "B": B, "what": what, "bytes_total": bytes_total, "engine": eng,
         "value": payload / elapsed / 2**30,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "verified": ok and bad == 0.0,
+        "rank": {"ms_per_step": round(own_elapsed * 1e3 / args.steps, 4), "encode_ms": round(enc_ms, 4),
+                 "decode_ms": round(dec_ms, 4), "verified": bool(ok)},
         "kernel_ms_per_step": enc_ms + dec_ms,
         "host_enqueue_us": {"encode": round(host[0] / args.steps * 1e6, 2),
                             "decode": round(host[1] / args.steps * 1e6, 2),
@@ -457,7 +519,9 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
             "unit": "GB/s",
             "frac": round(enc_gbps / HBM_PEAK_GBPS, 4),
             "traffic": enc_traffic,
-            "kernel": f"combine_kernel<{k},{m},{'LdsEngine' if eng == 'lds' else 'PermEngine'},"
+            "traffic_stale": enc_stale,
+            "kernel_code_id": this_code_id(),
+            "kernel": f"combine_kernel<{k},{m},{'LdsEngine' if eng['encode'] == 'lds' else 'PermEngine'},"
                       "kAccNone,exact> (cec_encode)",
             "algorithmic_bytes_per_launch": enc_bytes,
             "launch_ms": round(enc_ms, 4),
@@ -467,6 +531,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
             "achieved": round(dec_gbps, 1), "frac": round(dec_gbps / HBM_PEAK_GBPS, 4),
             "algorithmic_bytes_per_launch": dec_bytes, "launch_ms": round(dec_ms, 4),
             "launch_ms_median": round(statistics.median(dec_t), 4), "traffic": dec_traffic,
+            "traffic_stale": dec_stale,
         },
     }
 
@@ -498,7 +563,7 @@ def measure_strong(torch, dist, ec, world, rank, args, whole):
         lo, hi = shard_stripes(stripes, rank, world)
         r = measure_device(torch, dist, ec, world, rank, args.workload, args, share=(lo, hi))
         out = point(r, hi - lo, world)
-        out.update(value=round(r["value"], 2), unit="GiB/s",
+        out.update(value=round(r["value"], 2), unit="GiB/s", rank=dict(r["rank"], stripes=[lo, hi]),
                    split=f"contiguous split of the {B} stripes over {world} GPUs (shard_stripes: by "
                          "count, by bytes for mixed sizes), max over ranks")
         return out
@@ -535,8 +600,10 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
     plan = ec.Plan([(s * n, s * n, n, src[s]) for s in range(B)])
     stream = torch.cuda.current_stream()
     ec.encode_region(k, m, mat, data, parity, T, stream)
-    for w in range(args.warmup):
+    warm = max(1, args.warmup)
+    for w in range(warm):
         ec.diff_update(k, m, mat, data, stage[w % 2], parity, True, plan, stream)
+    eng = engine_ran(ec)  # the library's own report of the engine the op ran with
     evs = [ec.Event() for _ in range(args.steps + 1)]
     torch.cuda.synchronize()
     if world > 1:
@@ -545,7 +612,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
     t0 = time.perf_counter()
     evs[0].record(stream)
     for s in range(args.steps):
-        ec.diff_update(k, m, mat, data, stage[(args.warmup + s) % 2], parity, True, plan, stream)
+        ec.diff_update(k, m, mat, data, stage[(warm + s) % 2], parity, True, plan, stream)
         evs[s + 1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -553,7 +620,8 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         dist.barrier()
     du_t = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
     ms = sum(du_t) / args.steps
-    lds = engine_of(ec, True) == "lds"
+    lds = eng == "lds"
+    own_elapsed = elapsed
     chk = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
     ec.encode_region(k, m, mat, data, chk, T, stream)
     torch.cuda.synchronize()
@@ -563,6 +631,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
     del ar, data, parity, stage, chk
     nbytes = (2 + 2 * m + 1) * T  # read old, new, M parities; write M parities + install
     gbps = nbytes / (ms * 1e-3) / 1e9
+    traffic, stale = load_traffic("rs32_diff_update", ("diff_update",), eng)
     return {
         "value": round(T * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s",
         "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
@@ -572,9 +641,11 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
                      "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(du_t), 4),
                      "kernel": f"combine_kernel<2,3,{'LdsEngine' if lds else 'PermEngine'},kAccAllButLast,exact> "
                                "(cec_diff_update, install)",
-                     "traffic": load_traffic("rs32_diff_update", ("diff_update",), "lds" if lds else "perm")[0]},
-        "engine": "lds" if lds else "perm",
+                     "traffic": traffic[0], "traffic_stale": stale},
+        "engine": eng,
         "verified": bool(ok and bad == 0.0),
+        "rank": {"ms_per_step": round(own_elapsed * 1e3 / args.steps, 4), "launch_ms": round(ms, 4),
+                 "verified": bool(ok)},
     }
 
 
@@ -600,8 +671,9 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
         mask = ec.recovery_mask(k, m, leader, [int(i != lost) for i in range(k + m)])
         outs = [out if j == lost else None for j in range(k)]
         out.zero_()
-        for _ in range(args.warmup):
+        for _ in range(max(1, args.warmup)):
             ec.decode(k, m, mat, [mask], data + parity, outs, plan, stream)
+        eng = engine_ran(ec)
         evs = [ec.Event() for _ in range(args.steps + 1)]
         torch.cuda.synchronize()
         if world > 1:
@@ -619,6 +691,7 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
         ts = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
         ms = sum(ts) / args.steps
         ok = bool(torch.equal(out, data[lost]))
+        own_elapsed = elapsed
         elapsed, bad = max_over_ranks([elapsed, 0.0 if ok else 1.0], dist)
         dec_bytes = (k + 1) * T  # read K survivors, write the rebuilt shard
         gbps = dec_bytes / (ms * 1e-3) / 1e9
@@ -626,11 +699,13 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
             "value": round(n * B * world * args.steps / elapsed / 2**30, 2), "unit": "GiB/s rebuilt",
             "mask": mask, "launch_ms": round(ms, 4), "launch_ms_median": round(statistics.median(ts), 4),
             "decode_frac": round(gbps / HBM_PEAK_GBPS, 4), "achieved_GBps": round(gbps, 1),
-            "algorithmic_bytes_per_launch": dec_bytes, "verified": ok and bad == 0.0,
+            "algorithmic_bytes_per_launch": dec_bytes, "verified": ok and bad == 0.0, "engine": eng,
+            "rank": {"ms_per_step": round(own_elapsed * 1e3 / args.steps, 4), "launch_ms": round(ms, 4),
+                     "verified": ok},
         }
     plan.destroy()
     del ar, data, parity, out
-    return {"workload": EXTRA_WORKLOADS["rs32_1m_recovery"], "cases": cases, "engine": engine_of(ec, True),
+    return {"workload": EXTRA_WORKLOADS["rs32_1m_recovery"], "cases": cases, "engine": eng,
             "value": min(c["value"] for c in cases.values()), "unit": "GiB/s rebuilt (slower case)",
             "decode_frac": min(c["decode_frac"] for c in cases.values()),
             "verified": all(c["verified"] for c in cases.values())}
@@ -740,6 +815,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
         dist.barrier()
     h2d, d2h = pcie_raw(torch)
     floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
+    own = el
     el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
     out = {
         "value": round(e.payload * world * steps / el / 2**30, 2), "unit": "GiB/s",
@@ -750,6 +826,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
         "pcie_GBps_raw": {"h2d": round(h2d, 1), "d2h": round(d2h, 1)},
         "h2d_bytes_per_step": e.h2d_bytes, "d2h_bytes_per_step": e.d2h_bytes,
         "verified": bool(ok and bad == 0.0),
+        "rank": {"ms_per_step": round(own * 1e3 / steps, 3), "verified": bool(ok)},
     }
     e.close()
     return out
@@ -770,9 +847,9 @@ def run_device(args):
     also = {}
     for w in [x for x in args.also.split(",") if x and x != args.workload]:
         torch.cuda.empty_cache()
-        if w in ("rs32_diff_update", "rs32_diff_update_perm"):
-            if w == "rs32_diff_update_perm":
-                ec.set_engine(ec.CEC_ENGINE_PERM)
+        if w in ("rs32_diff_update", "rs32_diff_update_lds"):
+            if w == "rs32_diff_update_lds":
+                ec.set_engine(ec.CEC_ENGINE_LDS)
             try:
                 also[w] = measure_diff_update(torch, dist, ec, world, rank, args)
             finally:
@@ -799,10 +876,19 @@ def run_device(args):
             "engine": o["engine"],
             "encode_frac": o["roofline"]["frac"], "decode_frac": o["decode_roofline"]["frac"],
             "encode_ms": o["roofline"]["launch_ms"], "decode_ms": o["decode_roofline"]["launch_ms"],
-            "verified": o["verified"],
+            "verified": o["verified"], "rank": o["rank"],
         }
         if w == "rs32_4k_lds":
             also[w]["kernel"] = o["roofline"]["kernel"]
+    # per-rank evidence, outside every timed region: device identity and own times
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+            "identity": device_identity(torch, torch.cuda.current_device()),
+            "weak": r["rank"], "strong": strong.pop("rank", None) if strong else None,
+            "other_workloads": {w: v.pop("rank", None) for w, v in also.items()}}
+    for v in also.values():  # the recovery cases carry theirs per case
+        for c in v.get("cases", {}).values():
+            c.pop("rank", None)
+    ranks = ranks_summary(gather_ranks(dist, mine), dist.get_backend() if world > 1 else "none")
     if rank == 0:
         k, m, n, B = r["k"], r["m"], r["n"], r["B"]
         res = {
@@ -824,13 +910,15 @@ def run_device(args):
                 "k": k, "m": m, "value_bytes": n or "mixed", "stripes_per_gpu": B,
                 "bytes_per_shard_per_gpu": r["bytes_total"],
                 "parallelism": f"{world} x independent stripe batches, no collective",
-                "engine": args.engine if args.engine != "auto" else
-                          f"auto ({r['engine'].upper()} for this workload's encode and decode; LDS for the "
-                          "diff-update, single-mask decodes and values of 64 KiB and more)",
+                "engine": (args.engine if args.engine != "auto" else "auto") +
+                          f" (ran: encode {r['engine']['encode'].upper()}, decode {r['engine']['decode'].upper()}, "
+                          "as cec_last_engine reports; AUTO = LDS for single-mask decodes and decodes of "
+                          "values of 64 KiB and more, PERM for every other op)",
             },
             "roofline": r["roofline"],
             "decode_roofline": r["decode_roofline"],
             "verified": r["verified"] and all(v["verified"] for v in also.values()),
+            "ranks": ranks,
         }
         if strong is not None:
             res["strong"] = strong
@@ -1211,11 +1299,20 @@ def run_harness_check(args):
         dist.all_gather_object(spans, (rank, lo, hi))
     else:
         spans = [(0, lo, hi)]
+    # the per-rank evidence block of the device line, with a CPU stand-in for the device
+    # identity: the process, or one shared "device" when CEC_BENCH_DEVICE pins every rank
+    # to one (as it pins every GPU rank to one card)
+    shared = os.environ.get("CEC_BENCH_DEVICE")
+    ident = {"device": shared or f"cpu-process-{os.getpid()}", "name": "cpu stand-in", "arch": None,
+             "pci": None, "uuid": f"cpu-{shared}" if shared else f"cpu-{os.getpid()}"}
+    mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "identity": ident,
+            "weak": {"ms_per_step": round(elapsed * 1e3, 4), "stripes": [lo, hi]}, "strong": None}
+    ranks = ranks_summary(gather_ranks(dist if world > 1 else None, mine), "gloo" if world > 1 else "none")
     if rank == 0:
         print(json.dumps({"harness_check": True, "n_gpus": world, "gpus_arg": args.gpus,
                           "elapsed_max": got[0], "slowest_sleep": got[1], "max_rank": got[2],
                           "shards": spans, "local_rank_env": os.environ.get("LOCAL_RANK"),
-                          "backend": "gloo"}), flush=True)
+                          "backend": "gloo", "ranks": ranks}), flush=True)
 
 
 def main(argv=None):

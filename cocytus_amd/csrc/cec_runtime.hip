@@ -74,12 +74,17 @@ static DevInfo g_dev[64];
 static std::atomic<int> g_engine{CEC_ENGINE_AUTO};
 
 // The engine an op runs with, read once per op (its tables and its kernel must agree):
-// the process-wide setting, or under AUTO the one measured faster for the op --
-// `lds_op` for the fused diff-update and the single-mask decode, PERM for the others
-// (cocytus_ec.h).
+// the process-wide setting, or under AUTO the LDS engine only where it led PERM by more
+// than 2 % on the median of the recorded boxes -- `lds_op`: a decode with one mask for
+// the whole batch, or of values of 64 KiB and more -- and PERM for every other op
+// (cocytus_ec.h; DESIGN.md §4 "Engine per op").  Recorded per thread for
+// cec_last_engine().
+static thread_local int t_last_engine = -1;
 static int op_engine(bool lds_op) {
     const int e = g_engine.load();
-    return e == CEC_ENGINE_AUTO ? (lds_op ? CEC_ENGINE_LDS : CEC_ENGINE_PERM) : e;
+    const int r = e == CEC_ENGINE_AUTO ? (lds_op ? CEC_ENGINE_LDS : CEC_ENGINE_PERM) : e;
+    t_last_engine = r;
+    return r;
 }
 
 static int current_device(int *dev) {
@@ -159,10 +164,11 @@ static void launch_k(const CombineArgsN<S> &a, int grid, size_t lds, hipStream_t
 }
 
 // The 1 x 1 shapes (region multiply-XOR / write, parity apply) with the two-slot
-// arguments, for launches whose patterns use slots 0 and 1 only.
-template <class Eng>
-static bool launch_narrow(int acc, const CombineArgs &w, int grid, size_t lds, hipStream_t s) {
+// arguments, for launches whose patterns use slots 0 and 1 only.  narrow_args builds the
+// argument block they are passed (the launch-time check reads the same block).
+static CombineArgsN<kNarrowStreams> narrow_args(const CombineArgs &w) {
     CombineArgsN<kNarrowStreams> a;
+    memset(&a, 0, sizeof a);
     for (int i = 0; i < kNarrowStreams; ++i) a.base[i] = w.base[i];
     a.tiles = w.tiles;
     a.patterns = w.patterns;
@@ -172,7 +178,12 @@ static bool launch_narrow(int acc, const CombineArgs &w, int grid, size_t lds, h
     a.split_shift = w.split_shift;
     a.grid = w.grid;
     a.flags = w.flags;
-    const bool rel = (w.flags & kFlagSysRelease) != 0;
+    return a;
+}
+
+template <class Eng>
+static bool launch_narrow(int acc, const CombineArgsN<kNarrowStreams> &a, int grid, size_t lds, hipStream_t s) {
+    const bool rel = (a.flags & kFlagSysRelease) != 0;
     if (acc == kAccAll && rel) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams, true>(a, grid, lds, s);
     else if (acc == kAccAll) launch_k<1, 1, Eng, kAccAll, true, kNarrowStreams>(a, grid, lds, s);
     else if (acc == kAccNone && rel) launch_k<1, 1, Eng, kAccNone, true, kNarrowStreams, true>(a, grid, lds, s);
@@ -315,6 +326,16 @@ CEC_API int cec_plan_destroy(cec_plan *p) {
     return rc;
 }
 
+// The caller is destroying `stream`: wait for this plan's work on it and stop tracking it
+// (per-connection streams: the tracked list stays bounded by the streams alive).
+CEC_API int cec_plan_release_stream(cec_plan *p, void *stream) {
+    if (!p) return fail(CEC_EINVAL, "cec_plan_release_stream: plan is NULL");
+    if (hipError_t e = p->uses.release(p->device, static_cast<hipStream_t>(stream)); e != hipSuccess)
+        return fail(CEC_EHIP, "cec_plan_release_stream: %s", hipGetErrorString(e));
+    return CEC_OK;
+}
+CEC_API int cec_plan_tracked_streams(const cec_plan *p) { return p ? static_cast<int>(p->uses.size()) : 0; }
+
 CEC_API int cec_plan_create(cec_plan **out, const cec_extent *ext, int n, void *stream) {
     if (!out || n < 0 || (n > 0 && !ext)) return fail(CEC_EINVAL, "cec_plan_create: bad args");
     *out = nullptr;
@@ -422,15 +443,33 @@ static size_t occupancy_lds(int dev, uint32_t split_shift) {
 // most g_wt_max_bytes (reads + writes).  CEC_STORE_POLICY=nt|wt|auto and
 // CEC_WT_MAX_BYTES override (measurement).
 enum { kStoreAuto = 0, kStoreNt = 1, kStoreWt = 2 };
+// An unknown value (e.g. "WT") is reported on stderr once and ignored (auto).
 static const int g_store_policy = [] {
     const char *e = getenv("CEC_STORE_POLICY");
     if (!e || !*e || !strcmp(e, "auto")) return static_cast<int>(kStoreAuto);
-    return !strcmp(e, "wt") ? static_cast<int>(kStoreWt) : static_cast<int>(kStoreNt);
+    if (!strcmp(e, "wt")) return static_cast<int>(kStoreWt);
+    if (!strcmp(e, "nt")) return static_cast<int>(kStoreNt);
+    fprintf(stderr, "libcocytus_ec: CEC_STORE_POLICY=%s is not nt, wt or auto; using auto\n", e);
+    return static_cast<int>(kStoreAuto);
 }();
 static const uint64_t g_wt_max_bytes = [] {
+    const uint64_t dflt = uint64_t(512) << 20;
     const char *e = getenv("CEC_WT_MAX_BYTES");
-    return e && *e ? strtoull(e, nullptr, 0) : (uint64_t(512) << 20);
+    if (!e || !*e) return dflt;
+    char *end = nullptr;
+    const unsigned long long v = strtoull(e, &end, 0);
+    if (!end || *end) {
+        fprintf(stderr, "libcocytus_ec: CEC_WT_MAX_BYTES=%s is not a byte count; using %llu\n", e,
+                static_cast<unsigned long long>(dflt));
+        return dflt;
+    }
+    return static_cast<uint64_t>(v);
 }();
+// The store policy in force (tests: every kernel kind runs under each).
+CEC_API int cec_internal_store_policy(uint64_t *wt_max_bytes) {
+    if (wt_max_bytes) *wt_max_bytes = g_wt_max_bytes;
+    return g_store_policy;
+}
 static bool write_through(uint64_t n_tiles, int streams) {
     if (g_store_policy != kStoreAuto) return g_store_policy == kStoreWt;
     return n_tiles * kTile * static_cast<uint64_t>(streams) <= g_wt_max_bytes;
@@ -468,26 +507,33 @@ static LaunchShape launch_shape(const std::vector<Pattern> &pats, const std::vec
 // name (NULL: all), for the stream check below.
 enum KernelKind { kKindNarrow, kKindExact, kKindGeneric };
 
-// Every stream a kernel of `kind` will dereference for each used pattern, read from the
-// argument slots it will see (two for the narrow kernels), is the stream the pattern
-// names, and is not NULL.  A mismatch is a library bug (or a NULL arena the op's checks
-// missed) that would fault the GPU: refuse the launch instead.
-static bool stream_layout_ok(const CombineArgs &a, KernelKind kind, const Streams &st, const Pattern *hpats,
-                             size_t n_pats, const std::vector<char> *used) {
-    const int slots = kind == kKindNarrow ? kNarrowStreams : kMaxStreams;
+// Launch-time check of the argument block a kernel of `kind` is passed: every stream
+// slot a used pattern names must be one the block carries (below 2 for the narrow
+// kernels, whose block is narrow_args' copy of the first two slots; below kMaxStreams
+// otherwise) and hold a non-NULL base there.  Which arena the op meant for each slot is
+// decided by the op itself (it fills the slots); this check catches a kernel choice or
+// an argument block that cannot serve the patterns -- a slot the kernel's block does not
+// have, or an empty one -- which would otherwise fault the GPU.  A failure is refused.
+static bool stream_layout_ok(const uint8_t *const *bases, int slots, const Pattern *hpats, size_t n_pats,
+                             const std::vector<char> *used) {
     for (size_t q = 0; q < n_pats; ++q) {
         if (used && (q >= used->size() || !(*used)[q])) continue;
         const Pattern &p = hpats[q];
-        for (int i = 0; i < p.n_in; ++i) {
-            const int slot = p.in_stream[i];
-            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[slot]) return false;
-        }
-        for (int l = 0; l < p.n_out; ++l) {
-            const int slot = p.out_stream[l];
-            if (slot >= slots || !a.base[slot] || a.base[slot] != st.base[slot]) return false;
-        }
+        for (int i = 0; i < p.n_in; ++i)
+            if (p.in_stream[i] >= slots || !bases[p.in_stream[i]]) return false;
+        for (int l = 0; l < p.n_out; ++l)
+            if (p.out_stream[l] >= slots || !bases[p.out_stream[l]]) return false;
     }
     return true;
+}
+
+static bool layout_ok_for(KernelKind kind, const CombineArgs &a, const Pattern *hpats, size_t n_pats,
+                          const std::vector<char> *used) {
+    if (kind == kKindNarrow) {
+        const CombineArgsN<kNarrowStreams> na = narrow_args(a);
+        return stream_layout_ok(na.base, kNarrowStreams, hpats, n_pats, used);
+    }
+    return stream_layout_ok(a.base, kMaxStreams, hpats, n_pats, used);
 }
 
 static int launch_combine(int dev, const Streams &st, const uint8_t *tables, size_t n_pats,
@@ -506,8 +552,8 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
             ? kKindNarrow
             : exact_k ? kKindExact : kKindGeneric;
     for (int i = 0; i < kMaxStreams; ++i) a.base[i] = st.base[i];
-    if (!stream_layout_ok(a, kind, st, hpats, n_pats, used))
-        return fail(CEC_EINVAL, "internal: a launch's stream layout does not match its patterns "
+    if (!layout_ok_for(kind, a, hpats, n_pats, used))
+        return fail(CEC_EINVAL, "internal: a launch's argument block cannot serve its patterns "
                                 "(kind %d, %d x %d); not launched", static_cast<int>(kind), sh.en, sh.el);
     if (plan) a.tiles = plan->d_tiles;
     else a.implicit_len = implicit_len;
@@ -528,8 +574,9 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
     a.grid = static_cast<uint32_t>(grid);
     bool ok;
     if (kind == kKindNarrow) {
-        ok = lds ? launch_narrow<LdsEngine>(sh.eacc, a, grid, lds_bytes, stream)
-                 : launch_narrow<PermEngine>(sh.eacc, a, grid, lds_bytes, stream);
+        const CombineArgsN<kNarrowStreams> na = narrow_args(a);
+        ok = lds ? launch_narrow<LdsEngine>(sh.eacc, na, grid, lds_bytes, stream)
+                 : launch_narrow<PermEngine>(sh.eacc, na, grid, lds_bytes, stream);
     } else if (kind == kKindExact) {
         ok = lds ? launch_exact<LdsEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream)
                  : launch_exact<PermEngine>(sh.en, sh.el, sh.eacc, a, grid, lds_bytes, stream);
@@ -691,6 +738,33 @@ CEC_API int cec_set_engine(cec_engine e) {
     return CEC_OK;
 }
 CEC_API cec_engine cec_get_engine(void) { return static_cast<cec_engine>(g_engine.load()); }
+CEC_API int cec_last_engine(void) { return t_last_engine; }
+
+// Test hook: the launch-time check (layout_ok_for) on one pattern, as launch_combine
+// runs it, for a narrow or a full argument block built from `bases`.  Host only.
+CEC_API int cec_internal_check_launch_layout(int narrow, const int *in_slots, int n_in, const int *out_slots,
+                                             int n_out, const void *const *bases, int n_bases) {
+    if (n_in < 0 || n_in > kPatN || n_out < 0 || n_out > kPatL || n_bases < 0 || n_bases > kMaxStreams ||
+        (n_in && !in_slots) || (n_out && !out_slots) || (n_bases && !bases))
+        return fail(CEC_EINVAL, "cec_internal_check_launch_layout: bad args");
+    Pattern p = blank_pattern();
+    p.n_in = n_in;
+    p.n_out = n_out;
+    for (int i = 0; i < n_in; ++i) {
+        if (in_slots[i] < 0 || in_slots[i] >= kMaxStreams) return fail(CEC_EINVAL, "slot %d", in_slots[i]);
+        p.in_stream[i] = static_cast<uint8_t>(in_slots[i]);
+    }
+    for (int l = 0; l < n_out; ++l) {
+        if (out_slots[l] < 0 || out_slots[l] >= kMaxStreams) return fail(CEC_EINVAL, "slot %d", out_slots[l]);
+        p.out_stream[l] = static_cast<uint8_t>(out_slots[l]);
+    }
+    CombineArgs a;
+    memset(&a, 0, sizeof a);
+    for (int i = 0; i < n_bases; ++i) a.base[i] = static_cast<uint8_t *>(const_cast<void *>(bases[i]));
+    if (!layout_ok_for(narrow ? kKindNarrow : kKindExact, a, &p, 1, nullptr))
+        return fail(CEC_EINVAL, "internal: a launch's argument block cannot serve its patterns; not launched");
+    return CEC_OK;
+}
 CEC_API int cec_set_waves_per_cu(int waves_per_cu) {
     if (waves_per_cu < 0 || waves_per_cu > 64) return fail(CEC_EINVAL, "bad waves_per_cu %d", waves_per_cu);
     g_waves_per_cu.store(waves_per_cu);
@@ -784,11 +858,12 @@ CEC_API int cec_region_multiply(const void *src, int multby, size_t nbytes, void
     return region_launch(dev, src, multby, nbytes, dst, add, static_cast<hipStream_t>(stream), false);
 }
 
-// AUTO's value-size rule for the encode and the decode: values of 64 KiB and more (and
-// contiguous regions) run the LDS engine, smaller ones PERM.  Measured on two boxes, two
-// rounds each (profiles/r03_evidence/engine_auto/workloads_box*/; a third box agreed): at 64 KiB, 1 MiB and
-// the mixed 256 B - 1 MiB batch the LDS engine led the encode by 0-1.6 % and the rotating
-// decode by 2.8-3.7 %; at 4 KiB the encode ties and PERM leads the rotating decode by 2-3 %.
+// AUTO's value-size rule for the decode: values of 64 KiB and more run the LDS engine,
+// smaller ones (with erasures varying per value) PERM.  Measured on two boxes, two rounds
+// each (profiles/r03_evidence/engine_auto/workloads_box*/; a third box agreed): at 64 KiB,
+// 1 MiB and the mixed 256 B - 1 MiB batch the LDS engine led the rotating decode by
+// 2.5-3.7 %, at 4 KiB PERM led it by 2-3 %.  The encode is within +-2 % at every size
+// (LDS ahead by 0-1.6 % on large values, a tie at 4 KiB), so it runs PERM throughout.
 static bool large_values(const cec_plan *plan) {
     return !plan || plan->total >= (uint64_t(64) << 10) * static_cast<uint64_t>(std::max(plan->n_ext, 1));
 }
@@ -817,7 +892,7 @@ static int encode_common(int k, int m, const int *matrix, const uint8_t *const *
         for (int j = 0; j < k; ++j) o.coef[j] = MATRIX(k + p, j);
         c.outs.push_back(o);
     }
-    return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream), nullptr, large_values(plan));
+    return run_combos(dev, st, {c}, plan, len, static_cast<hipStream_t>(stream));
 }
 
 // Ops with one pattern index every tile's pattern field into a one-entry table: it must be 0.
@@ -880,7 +955,9 @@ CEC_API int cec_diff_update(int k, int m, const int *matrix, uint8_t *const *dat
             c.outs.push_back(o);
         }
     }
-    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr, true);
+    // AUTO: PERM.  The LDS engine's diff-update was within +-3 % of PERM either way over
+    // the recorded boxes (median margin under 1 %; DESIGN.md §4 "Engine per op").
+    return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream));
 }
 
 CEC_API int cec_set_diff(int k, const uint8_t *const *data, const uint8_t *staging, uint8_t *diff,
@@ -1081,9 +1158,10 @@ CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, i
         }
     }
     // AUTO: one recovery mask for the whole batch (a server rebuilding one lid) runs the
-    // LDS engine (2-5 % ahead of PERM, profiles/r03_evidence/engine_auto/), and so do
-    // large values (large_values); erasures that vary per 4 KiB value run PERM (ahead by
-    // 2-3 % on the bench's rotating masks)
+    // LDS engine (2.2-4.8 % ahead of PERM with a non-unit leader inverse,
+    // profiles/r03_evidence/engine_auto/), and so do large values (large_values);
+    // erasures that vary per 4 KiB value run PERM (ahead by 2-3 % on the bench's
+    // rotating masks)
     return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr,
                       n_masks == 1 || large_values(plan));
 }

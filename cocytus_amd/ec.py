@@ -29,7 +29,7 @@ CEC_ENODEV = -6
 CEC_EFULL = -7
 CEC_ENGINE_PERM = 0
 CEC_ENGINE_LDS = 1
-CEC_ENGINE_AUTO = 2  # default: LDS for the diff-update, PERM for the other ops
+CEC_ENGINE_AUTO = 2  # default: LDS for single-mask and large-value decodes, PERM for the rest (cocytus_ec.h)
 CEC_MAX_K = 16
 CEC_MAX_M = 8
 UNIT_SIZE = 4096
@@ -99,6 +99,14 @@ _SIGS = {
     "cec_device_check": ([], _i),
     "cec_set_engine": ([_i], _i),
     "cec_get_engine": ([], _i),
+    "cec_last_engine": ([], _i),
+    "cec_internal_check_launch_layout": ([_i, _ip, _i, _ip, _i, _pp, _i], _i),
+    "cec_internal_store_policy": ([ctypes.POINTER(ctypes.c_uint64)], _i),
+    "cec_plan_release_stream": ([_vp, _vp], _i),
+    "cec_plan_tracked_streams": ([_vp], _i),
+    "cec_drainer_release_stream": ([_vp, _vp], _i),
+    "cec_recovery_release_stream": ([_vp, _vp], _i),
+    "cec_recovery_pool_release_stream": ([_vp, _vp], _i),
     "cec_set_waves_per_cu": ([_i], _i),
     "cec_get_waves_per_cu": ([], _i),
     "cec_plan_create": ([ctypes.POINTER(_vp), ctypes.POINTER(Extent), _i, _vp], _i),
@@ -215,6 +223,50 @@ def lib() -> ctypes.CDLL:
     return L
 
 
+def kernel_code_id(path: str | None = None) -> str | None:
+    """Identity of the library's device code: sha256 (16 hex digits) of its gfx950 code
+    object disassembled (llvm-objdump), one block per kernel sorted by name, addresses
+    and encodings dropped -- so host-only changes and a different link order of the same
+    kernels keep the id, and any change to a kernel's instructions changes it.  Nothing
+    is loaded.  None if the file or llvm-objdump is missing."""
+    import hashlib
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+
+    path = path or LIB_PATH
+    objdump = os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "llvm", "bin", "llvm-objdump")
+    if not (os.path.exists(path) and os.path.exists(objdump)):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        so = os.path.join(d, "lib.so")
+        shutil.copy(os.path.realpath(path), so)
+        if subprocess.run([objdump, "--offloading", so], cwd=d, capture_output=True).returncode:
+            return None
+        cos = sorted(f for f in os.listdir(d) if f.endswith("gfx950"))
+        if len(cos) != 1:
+            return None
+        r = subprocess.run([objdump, "-d", os.path.join(d, cos[0])], capture_output=True, text=True)
+        if r.returncode:
+            return None
+    funcs, cur = {}, None
+    for line in r.stdout.splitlines():
+        m = re.match(r"^[0-9a-f]+ <(\S+)>:$", line)
+        if m:
+            cur = funcs.setdefault(m.group(1), [])
+        elif cur is not None and line.startswith("\t"):
+            ins = line.split("//")[0].strip()
+            if ins:
+                cur.append(ins)
+    if not funcs:
+        return None
+    h = hashlib.sha256()
+    for name in sorted(funcs):
+        h.update(name.encode() + b"\n" + "\n".join(funcs[name]).encode() + b"\n\n")
+    return h.hexdigest()[:16]
+
+
 def _check(rc: int) -> None:
     if rc != CEC_OK:
         raise CecError(rc, lib().cec_last_error().decode(errors="replace"))
@@ -264,6 +316,26 @@ def set_engine(engine: int) -> None:
 
 def get_engine() -> int:
     return lib().cec_get_engine()
+
+
+def last_engine() -> int:
+    """cec_last_engine: the engine (CEC_ENGINE_PERM / _LDS) this thread's last op ran
+    with, AUTO resolved; -1 before the first op."""
+    return lib().cec_last_engine()
+
+
+def check_launch_layout(narrow: bool, in_slots, out_slots, bases) -> int:
+    """cec_internal_check_launch_layout (test hook, host only): CEC_OK or CEC_EINVAL."""
+    return lib().cec_internal_check_launch_layout(int(bool(narrow)), _int_array(in_slots), len(in_slots),
+                                                  _int_array(out_slots), len(out_slots), _ptr_array(bases),
+                                                  len(bases))
+
+
+def store_policy() -> tuple[str, int]:
+    """cec_internal_store_policy: ('auto' | 'nt' | 'wt', auto's write-through limit)."""
+    v = ctypes.c_uint64()
+    p = lib().cec_internal_store_policy(ctypes.byref(v))
+    return {0: "auto", 1: "nt", 2: "wt"}[p], int(v.value)
 
 
 def set_waves_per_cu(waves: int) -> None:
@@ -340,6 +412,14 @@ class Plan:
     @property
     def total_bytes(self) -> int:
         return lib().cec_plan_total_bytes(self.handle)
+
+    def release_stream(self, stream) -> None:
+        """cec_plan_release_stream: call before destroying a stream this plan was used on."""
+        _check(lib().cec_plan_release_stream(self.handle, _stream(stream)))
+
+    @property
+    def tracked_streams(self) -> int:
+        return lib().cec_plan_tracked_streams(self.handle)
 
     def destroy(self) -> None:
         if self._h:
@@ -450,6 +530,9 @@ class Drainer:
         addr = ctypes.cast(p, ctypes.c_void_p).value
         return addr, np.ctypeslib.as_array((ctypes.c_uint8 * cap.value).from_address(addr))
 
+    def release_stream(self, stream) -> None:
+        _check(lib().cec_drainer_release_stream(self._h, _stream(stream)))
+
     def destroy(self) -> None:
         if self._h:
             _check(lib().cec_drainer_destroy(self._h))
@@ -515,6 +598,9 @@ class Recovery:
                                                      for i in range(self.k + self.m)])
         oo = (ctypes.c_void_p * self.k)(*[_host_or_dev(out.get(j)) or None for j in range(self.k)])
         _check(lib().cec_recovery_finish(self._h, peer_lid, _host_or_dev(units), pr, oo, _stream(stream)))
+
+    def release_stream(self, stream) -> None:
+        _check(lib().cec_recovery_release_stream(self._h, _stream(stream)))
 
     def destroy(self) -> None:
         if self._h:
@@ -610,6 +696,9 @@ class RecoveryPool:
     @property
     def active(self) -> int:
         return int(lib().cec_recovery_pool_active(self._h))
+
+    def release_stream(self, stream) -> None:
+        _check(lib().cec_recovery_pool_release_stream(self._h, _stream(stream)))
 
     def destroy(self) -> None:
         if self._h:

@@ -21,6 +21,11 @@
  * its calls used and its destroy synchronises exactly those (never the whole device);
  * a handle of a destroyed stream cannot be synchronised (it crashes the HIP runtime).
  * This is a change from the first release, whose destroy waited for the whole device.
+ * The recorded list grows with every distinct stream an object is used on.  A long-lived
+ * object used on short-lived streams (one per client connection) calls its
+ * *_release_stream(obj, stream) before destroying such a stream: that waits for the
+ * object's work on it and drops it from the list, which then stays bounded by the
+ * streams alive (and the object's destroy no longer touches the dead handle).
  *
  * THREADS: every entry point may be called from any thread.  The library's shared
  * state (caches, the engine and occupancy settings) is thread-safe, and each op reads
@@ -85,11 +90,12 @@ typedef struct cec_plan cec_plan;
  * other.  PERM looks up three 8-entry byte tables per coefficient with v_perm_b32
  * (pure VALU, no LDS); LDS stages one 256-entry product row per coefficient,
  * exp[log x + log c] built from the log / antilog tables, in LDS (one ds_read_u8 per
- * byte).  AUTO (default) picks per op the engine measured faster for it:
- * LDS for the fused diff-update (cec_diff_update), for a decode with one mask for the
- * whole batch (cec_decode, n_masks == 1), and for encodes and decodes of values of
- * 64 KiB and more (a plan's mean extent; cec_encode_region always); PERM for every
- * other op, including encodes and per-value rotating decodes of smaller values. */
+ * byte).  AUTO (default) runs the LDS engine only where it led PERM by more than 2 % on
+ * the median of the recorded boxes: cec_decode with one mask for the
+ * whole batch (n_masks == 1), or of values of 64 KiB and more (the plan's mean extent).
+ * Every other op runs PERM: encodes (any size), per-value rotating decodes of smaller
+ * values, the diff-update, residual, solve, set diff, apply, region multiply and the
+ * recovery sessions and pool. */
 typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1, CEC_ENGINE_AUTO = 2 } cec_engine;
 
 /* ---- runtime ---- */
@@ -98,6 +104,9 @@ const char *cec_last_error(void);               /* thread-local message of the l
 int cec_device_check(void);                     /* CEC_OK if the current device is gfx950 */
 int cec_set_engine(cec_engine e);               /* process-wide; default CEC_ENGINE_AUTO */
 cec_engine cec_get_engine(void);
+/* The engine (CEC_ENGINE_PERM or CEC_ENGINE_LDS) the calling thread's last op chose
+ * (AUTO resolved), -1 before its first op.  Diagnostics: which kernel family ran. */
+int cec_last_engine(void);
 /* Occupancy of the streaming kernels: at most waves_per_cu waves of one launch per CU
  * (0 = as many as fit).  Process-wide; the initial value comes from the
  * CEC_WAVES_PER_CU environment variable.  A tuning knob: every value is bit-exact. */
@@ -127,6 +136,11 @@ int cec_plan_create(cec_plan **out, const cec_extent *extents, int n, void *stre
  * sessions, drainers, pools) before the streams they were used on.  A plan used inside
  * a captured graph must outlive the graph's replays. */
 int cec_plan_destroy(cec_plan *plan);
+/* Before destroying `stream`: wait for this plan's work on it and stop tracking it
+ * (LIFETIME RULE above).  Not used on it: no-op.  cec_plan_tracked_streams: how many
+ * streams the plan's destroy would synchronise now. */
+int cec_plan_release_stream(cec_plan *plan, void *stream);
+int cec_plan_tracked_streams(const cec_plan *plan);
 int cec_plan_num_extents(const cec_plan *plan);
 int64_t cec_plan_num_tiles(const cec_plan *plan);
 uint64_t cec_plan_total_bytes(const cec_plan *plan); /* sum of extent lengths */
@@ -211,6 +225,7 @@ typedef struct cec_drainer cec_drainer;
 int cec_drainer_create(cec_drainer **out, int k, int m, const int *matrix, int lid_self,
                        size_t staging_bytes);
 int cec_drainer_destroy(cec_drainer *d);
+int cec_drainer_release_stream(cec_drainer *d, void *stream);   /* LIFETIME RULE, top */
 
 /* parity[addr..] ^= MATRIX(lid_self, src_lid) * buf for every update, as the sequential
  * loop of memcached.c:7762-7767 would leave it (XOR accumulation commutes; updates
@@ -247,6 +262,7 @@ int cec_recovery_create(cec_recovery **out, int k, int m, const int *matrix, int
                         const uint8_t *parity_arena /* device: this parity's arena */,
                         void *stream);
 int cec_recovery_destroy(cec_recovery *r);
+int cec_recovery_release_stream(cec_recovery *r, void *stream); /* LIFETIME RULE, top */
 
 /* recovery_recover_units (recovery.c:61-96): data peer peer_lid (in mask, not yet
  * applied) sent its raw bytes of the whole range (nbuf bytes).  The first peer also
@@ -296,6 +312,7 @@ typedef struct cec_recovery_pool cec_recovery_pool;
 int cec_recovery_pool_create(cec_recovery_pool **out, int k, int m, const int *matrix, int lid_self,
                              const uint8_t *parity_arena /* device */, int capacity_units);
 int cec_recovery_pool_destroy(cec_recovery_pool *pool);
+int cec_recovery_pool_release_stream(cec_recovery_pool *pool, void *stream); /* LIFETIME RULE */
 /* start_recovery / do_recovery: returns the request id (>= 0), CEC_EFULL when the pool
  * has no unit_end - unit_begin + 1 free contiguous units, or CEC_EINVAL. */
 int cec_recovery_pool_begin(cec_recovery_pool *pool, uint32_t mask, int unit_begin, int unit_end);
@@ -369,6 +386,19 @@ typedef struct cec_sync_record {
     int fenced;             /* a system-scope fence ran behind the op (fence event or stream sync) */
 } cec_sync_record;
 int cec_last_sync(cec_sync_record *out);
+
+/* ---- test hooks (host only, launch nothing; not for servers) ----
+ * cec_internal_check_launch_layout: the launch-time check every op's launch runs, on one
+ * pattern reading in_slots and writing out_slots, against the kernel argument block built
+ * from bases[0..n_bases) -- the two-slot block of the narrow 1 x 1 kernels (narrow != 0)
+ * or the full one.  CEC_OK, or CEC_EINVAL where the launch would be refused (a slot the
+ * block does not carry, or a NULL base).
+ * cec_internal_store_policy: the store policy parsed from CEC_STORE_POLICY (0 auto,
+ * 1 non-temporal, 2 write-through; unknown values warn once and mean auto) and, in
+ * *wt_max_bytes, auto's write-through limit (CEC_WT_MAX_BYTES, default 512 MiB). */
+int cec_internal_check_launch_layout(int narrow, const int *in_slots, int n_in, const int *out_slots,
+                                     int n_out, const void *const *bases, int n_bases);
+int cec_internal_store_policy(uint64_t *wt_max_bytes);
 
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ----
  * Events are for timing: recorded without the system-scope fence, so waiting on one

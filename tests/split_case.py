@@ -1,9 +1,13 @@
-"""Parity of every launch shape under a pinned workgroups-per-tile choice.
+"""Parity of every launch shape under a pinned workgroups-per-tile choice or store policy.
 
 Run as a child process by tests/test_gpu_parity.py::test_forced_split_shift with
-CEC_SPLIT_SHIFT set (the library reads it once per process).  Covers aligned full
-tiles, ragged / misaligned tiles, RMW outputs and the implicit region, against the
-oracle.  Prints "OK" on success; any mismatch raises.
+CEC_SPLIT_SHIFT set, and by ::test_store_policy_every_kernel_kind with CEC_STORE_POLICY /
+CEC_WT_MAX_BYTES set (the library reads them once per process; CEC_EXPECT_POLICY names
+the policy the child must see).  Covers every kernel kind -- the narrow 1 x 1 kernels
+(region multiply), exact shapes (encode, decode, diff-update) and the capacity kernel
+(RS(12,4): 12 inputs) -- on aligned full tiles, ragged / misaligned tiles, RMW outputs
+and the implicit region, against the oracle, both engines.  Prints "OK" on success;
+any mismatch raises.
 """
 from __future__ import annotations
 
@@ -23,6 +27,10 @@ def main() -> None:
     from cocytus_amd import ec
 
     assert ec.device_check() == ec.CEC_OK, ec.lib().cec_last_error()
+    want = os.environ.get("CEC_EXPECT_POLICY")
+    if want:
+        policy, limit = ec.store_policy()
+        assert f"{policy}:{limit}" == want, (policy, limit, want)
     for engine in (ec.CEC_ENGINE_LDS, ec.CEC_ENGINE_PERM):  # both GF engines per split
         ec.set_engine(engine)
         check(torch, ec)
@@ -98,6 +106,21 @@ def check(torch, ec) -> None:
         want = dst.copy()
         pyoracle.region_multiply(src[shift:shift + n].copy(), 0x53, want[shift:shift + n], 1)
         assert np.array_equal(dd.cpu().numpy(), want), f"region shift {shift}"
+
+    # the capacity (generic) kernel: RS(12, 4), 12 inputs > the exact shapes' 8
+    k2, m2 = 12, 4
+    mat2 = ec.coding_matrix(k2, m2)
+    n2 = 5 * 4096 + 333
+    host2 = [rng.integers(0, 256, n2, dtype=np.uint8) for _ in range(k2)]
+    par2 = [torch.zeros(n2, dtype=torch.uint8, device="cuda") for _ in range(m2)]
+    with ec.Plan([(0, 0, 4 * 4096, 0), (4 * 4096 + 16, 0, 4096 + 300, 0)]) as gp:
+        ec.encode(k2, m2, mat2, [dev(h) for h in host2], par2, gp)
+    torch.cuda.synchronize()
+    full2 = pyoracle.encode(mat2, k2, m2, host2)
+    for p in range(m2):
+        got = par2[p].cpu().numpy()
+        assert np.array_equal(got[:4 * 4096], full2[p][:4 * 4096]), f"generic parity {p}"
+        assert np.array_equal(got[4 * 4096 + 16:n2 - 17], full2[p][4 * 4096 + 16:n2 - 17]), f"generic parity {p}"
 
 
 if __name__ == "__main__":

@@ -149,11 +149,14 @@ def test_arena_stride_is_odd_pages(lib):
 
 
 def test_default_engine_is_auto(lib):
-    """The product default is AUTO: per op the engine measured faster for it, LDS for the
-    fused diff-update, PERM for the others.  PERM and LDS stay selectable
-    and both are in every GPU parity test; AUTO is what every test that leaves the engine
-    alone runs."""
+    """The product default is AUTO: the LDS engine only where it led PERM by more than 2 %
+    on the median of the recorded boxes -- cec_decode with one mask for the batch, or of
+    values of 64 KiB and more -- and PERM for every other op (cocytus_ec.h, DESIGN.md §4;
+    the choices themselves are asserted on the GPU, test_auto_engine_choices).  PERM and
+    LDS stay selectable and both are in every GPU parity test; AUTO is what every test
+    that leaves the engine alone runs."""
     assert lib.get_engine() == lib.CEC_ENGINE_AUTO
+    assert lib.last_engine() == -1  # no op has run on this thread
     for e in (lib.CEC_ENGINE_PERM, lib.CEC_ENGINE_LDS, lib.CEC_ENGINE_AUTO):
         lib.set_engine(e)
         assert lib.get_engine() == e
@@ -240,3 +243,84 @@ def test_release_epilogue_in_gfx950_code(lib, tmp_path):
             while ins[k] == "s_waitcnt vmcnt(0)":
                 k -= 1
             assert k < e - 1 and ins[k] == "buffer_wbl2 sc0 sc1", (f, ins[max(0, e - 6):e + 1])
+
+
+def test_launch_layout_check_refuses(lib):
+    """The launch-time check (cocytus_ec.h test hook, the very function every launch runs):
+    a pattern naming a stream slot the kernel's argument block does not carry -- slot 2 on
+    the two-slot narrow 1 x 1 kernels -- or a slot whose base is NULL is refused with
+    CEC_EINVAL before anything is launched (no device needed); a block that serves the
+    pattern passes."""
+    a, b, c = 0x10000, 0x20000, 0x30000
+    ok, bad = lib.CEC_OK, lib.CEC_EINVAL
+    # narrow: two slots only
+    assert lib.check_launch_layout(True, [0], [1], [a, b]) == ok
+    assert lib.check_launch_layout(True, [0], [2], [a, b, c]) == bad  # slot 2 is not in the block
+    assert lib.check_launch_layout(True, [2], [1], [a, b, c]) == bad
+    assert lib.check_launch_layout(True, [0], [1], [a, None]) == bad  # NULL output base
+    # the full block: every slot the pattern names must hold a base
+    assert lib.check_launch_layout(False, [0, 1, 2], [3, 4], [a, b, c, a + 1, b + 1]) == ok
+    assert lib.check_launch_layout(False, [0, 1, 2], [3, 5], [a, b, c, a + 1, b + 1]) == bad
+    assert lib.check_launch_layout(False, [0, 9], [3], [a, b, c, a + 1]) == bad
+    assert "not launched" in lib.lib().cec_last_error().decode()
+
+
+def _policy_in_child(env_extra):
+    env = dict(os.environ)
+    for k in ("CEC_STORE_POLICY", "CEC_WT_MAX_BYTES"):
+        env.pop(k, None)
+    env.update(env_extra)
+    code = ("import sys, json; sys.path.insert(0, %r)\nfrom cocytus_amd import ec\n"
+            "print(json.dumps(ec.store_policy()))\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stderr
+    import json
+
+    return tuple(json.loads(r.stdout.strip().splitlines()[-1])), r.stderr
+
+
+def test_store_policy_environment(lib):
+    """CEC_STORE_POLICY / CEC_WT_MAX_BYTES (measurement overrides of the per-launch store
+    policy): nt, wt and auto are taken; anything else (e.g. "WT") is reported
+    on stderr and means auto, instead of silently selecting non-temporal stores."""
+    assert _policy_in_child({}) == (("auto", 512 << 20), "")
+    assert _policy_in_child({"CEC_STORE_POLICY": "nt"})[0] == ("nt", 512 << 20)
+    assert _policy_in_child({"CEC_STORE_POLICY": "wt"})[0] == ("wt", 512 << 20)
+    assert _policy_in_child({"CEC_WT_MAX_BYTES": "0"})[0] == ("auto", 0)
+    got, err = _policy_in_child({"CEC_STORE_POLICY": "WT"})
+    assert got == ("auto", 512 << 20) and "CEC_STORE_POLICY=WT" in err
+    got, err = _policy_in_child({"CEC_WT_MAX_BYTES": "lots"})
+    assert got == ("auto", 512 << 20) and "CEC_WT_MAX_BYTES=lots" in err
+
+
+@pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="llvm-objdump not in this image")
+def test_kernel_code_id(lib):
+    """ec.kernel_code_id: a stable identity of the library's gfx950 kernels (their
+    disassembly, by name), the key bench.py uses to decide whether the committed PMC
+    traffic still describes the kernels it runs."""
+    a = lib.kernel_code_id()
+    assert a and re.fullmatch(r"[0-9a-f]{16}", a)
+    assert lib.kernel_code_id() == a
+    assert lib.kernel_code_id("/nonexistent/lib.so") is None
+
+
+def test_roofline_traffic_tied_to_the_build(tmp_path, monkeypatch):
+    """bench.py reports roofline.traffic from profiles/pmc_traffic*.json only while the
+    summary's recorded kernel_code_id equals the library's; otherwise (or with no record)
+    traffic is null and traffic_stale is true."""
+    import json
+
+    import bench
+
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    doc = {"rs32_4k": {"encode_hbm_bytes_per_launch": 11.0, "decode_hbm_bytes_per_launch": 22.0},
+           "_build": {"kernel_code_id": "00112233aabbccdd"}}
+    (prof / "pmc_traffic.json").write_text(json.dumps(doc))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.load_traffic("rs32_4k", code_id="00112233aabbccdd") == ((11.0, 22.0), False)
+    assert bench.load_traffic("rs32_4k", code_id="ffffffffffffffff") == ((None, None), True)
+    assert bench.load_traffic("rs32_4k", ("encode",), "lds", code_id="00112233aabbccdd") == ((None,), True)
+    del doc["_build"]
+    (prof / "pmc_traffic.json").write_text(json.dumps(doc))
+    assert bench.load_traffic("rs32_4k", code_id="00112233aabbccdd") == ((None, None), True)

@@ -104,6 +104,40 @@ def test_bench_self_launches_ranks(world):
     assert out["max_rank"] == world - 1  # the slowest rank's numbers are the ones reported
     assert out["slowest_sleep"] == pytest.approx(0.01 * world)
     assert out["elapsed_max"] >= 0.01 * world
+    # the per-rank evidence block the device line carries (the N > 1 line shows
+    # on its own which devices ran and which rank straggled)
+    rk = out["ranks"]
+    assert rk["world_size"] == world and rk["backend"] == "gloo"
+    assert rk["distinct_devices"] is True
+    assert [e["rank"] for e in rk["per_rank"]] == list(range(world))
+    assert rk["slowest_rank_weak"] == world - 1
+    assert [e["weak"]["stripes"] for e in rk["per_rank"]] == [[q * per, (q + 1) * per] for q in range(world)]
+    assert max(e["weak"]["ms_per_step"] for e in rk["per_rank"]) == pytest.approx(out["elapsed_max"] * 1e3, rel=1e-3)
+
+
+def test_bench_ranks_on_one_device_are_not_distinct():
+    """CEC_BENCH_DEVICE pins every rank to one device (the one-card rehearsal): the line
+    says so (distinct_devices false) instead of passing for an N-GPU run."""
+    import json
+
+    r = _run_bench(["--gpus", "2", "--harness-check"], env_extra={"CEC_BENCH_DEVICE": "0"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    rk = json.loads(r.stdout.strip().splitlines()[-1])["ranks"]
+    assert rk["world_size"] == 2 and rk["distinct_devices"] is False
+
+
+def test_ranks_summary():
+    import bench
+
+    def e(rank, uuid, pci, weak, strong=None):
+        return {"rank": rank, "identity": {"uuid": uuid, "pci": pci}, "weak": {"ms_per_step": weak},
+                "strong": None if strong is None else {"ms_per_step": strong}}
+
+    s = bench.ranks_summary([e(0, "u0", "0000:05:00", 1.0, 0.2), e(1, "u1", "0000:15:00", 1.2, 0.1)], "nccl")
+    assert s["distinct_devices"] and s["slowest_rank_weak"] == 1 and s["slowest_rank_strong"] == 0
+    s = bench.ranks_summary([e(0, "u0", "0000:05:00", 1.0), e(1, "u0", "0000:05:00", 0.5)], "gloo")
+    assert not s["distinct_devices"] and s["slowest_rank_weak"] == 0 and "slowest_rank_strong" not in s
+    assert bench.ranks_summary([e(0, "u0", "p", 1.0)], "none")["distinct_devices"]
 
 
 def test_bench_single_rank_runs_in_process():
@@ -208,7 +242,7 @@ def test_bench_arguments():
     assert (a.gpus, a.workload, a.engine) == (1, "rs32_4k", "auto")
     assert 1 <= a.steps <= 100 and a.warmup >= 1
     assert set(a.also.split(",")) == {"rs32_4k_lds", "rs32_mixed", "rs32_1m", "rs42_64k",
-                                      "rs32_1m_recovery", "rs32_diff_update", "rs32_diff_update_perm",
+                                      "rs32_1m_recovery", "rs32_diff_update", "rs32_diff_update_lds",
                                       "rs32_e2e"}
     assert not a.no_strong
     assert bench.parse(["--also="]).also == ""

@@ -201,3 +201,80 @@ def test_cfg2_full_batch_parity_vs_oracle(gpu, oracle):
     for q, j in enumerate(lost_of):
         sel = torch.arange(q, B, len(masks), device="cuda")
         assert torch.equal(out[j].view(B, n)[sel], data[j].view(B, n)[sel]), f"mask {q}"
+
+
+@pytest.fixture(scope="module")
+def cfg3_batch(gpu, oracle):
+    """BASELINE configs[2] at its stated size: bench.layout("rs32_mixed") -- 8,432 RS(3,2)
+    values, log-uniform 256 B - 1 MiB, ~1 GiB per shard, starts 16-B aligned
+    (ecalloc.c:176) -- with random data (generated on the device, seeded), the oracle's
+    parity of every value (AVX2 restatement, pinned to the scalar oracle on a sample), and
+    per arena byte the data shard the rotating decode rebuilds there (-1: the alignment
+    gaps between values, which no op may write)."""
+    import bench
+
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    stripes, arena = bench.layout("rs32_mixed")
+    assert len(stripes) == 8432 and sum(ln for _, ln in stripes) >= 1 << 30
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70003)
+    data = [torch.randint(0, 256, (arena,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    hostd = [d.cpu().numpy() for d in data]
+    probe, ref = np.zeros(3 * 4096 + 5, np.uint8), np.zeros(3 * 4096 + 5, np.uint8)
+    for j in range(k):  # the SIMD restatement == the scalar oracle on a sample
+        oracle.region_multiply_simd(hostd[j][:probe.size], mat[(k + 1) * k + j], probe)
+        oracle.region_multiply(hostd[j][:ref.size].copy(), mat[(k + 1) * k + j], ref, 1)
+    assert np.array_equal(probe, ref)
+    masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
+             for p in range(m) for j in range(k)]
+    lost_of = [[j for j in range(k) if not (mk >> j) & 1][0] for mk in masks]
+    label = np.full(arena, -1, np.int8)
+    for s, (o, ln) in enumerate(stripes):
+        label[o:o + ln] = lost_of[s % len(masks)]
+    exp = []
+    for p in range(m):
+        e = np.zeros(arena, np.uint8)
+        for j in range(k):
+            oracle.region_multiply_simd(hostd[j], mat[(k + p) * k + j], e)
+        e[label < 0] = 0  # gaps: never written (parity arena starts zeroed)
+        exp.append(dev(torch, e))
+    del hostd
+    return {"k": k, "m": m, "mat": mat, "stripes": stripes, "arena": arena, "data": data, "masks": masks,
+            "label": dev(torch, label), "exp": exp}
+
+
+@pytest.mark.parametrize("engine_name", ["auto", "perm", "lds"])
+def test_cfg3_mixed_full_size(gpu, cfg3_batch, engine_name):
+    """BASELINE configs[2] ("RS(3,2) encode + single-shard decode, mixed 256 B-1 MiB
+    values") at the size the bench runs it (bench.layout("rs32_mixed"), ~1 GiB per
+    shard): the whole batch's parity equals the oracle's byte for byte, and the rotating
+    single-shard decode (masks as start_recovery builds them, memcached.c:8136-8151;
+    residual + leader solve, recovery.c:61-96, memcached.c:7842-7922) rebuilds every
+    value's lost shard byte for byte and writes nothing else.  Under AUTO (the default;
+    PERM encode, LDS decode for this mean extent, as cec_last_engine reports), PERM and
+    LDS."""
+    torch, ec = gpu
+    c = cfg3_batch
+    k, m, mat, stripes, arena = c["k"], c["m"], c["mat"], c["stripes"], c["arena"]
+    default = ec.get_engine()
+    ec.set_engine({"auto": ec.CEC_ENGINE_AUTO, "perm": ec.CEC_ENGINE_PERM, "lds": ec.CEC_ENGINE_LDS}[engine_name])
+    try:
+        parity = [torch.zeros(arena, dtype=torch.uint8, device="cuda") for _ in range(m)]
+        out = [torch.zeros(arena, dtype=torch.uint8, device="cuda") for _ in range(k)]
+        with ec.Plan([(o, 0, ln, 0) for o, ln in stripes]) as ep, \
+             ec.Plan([(o, 0, ln, s % len(c["masks"])) for s, (o, ln) in enumerate(stripes)]) as dp:
+            ec.encode(k, m, mat, c["data"], parity, ep)
+            ran_enc = ec.last_engine()
+            ec.decode(k, m, mat, c["masks"], c["data"] + parity, out, dp)
+            ran_dec = ec.last_engine()
+            torch.cuda.synchronize()
+    finally:
+        ec.set_engine(default)
+    if engine_name == "auto":
+        assert (ran_enc, ran_dec) == (ec.CEC_ENGINE_PERM, ec.CEC_ENGINE_LDS)
+    for p in range(m):
+        assert torch.equal(parity[p], c["exp"][p]), f"parity {p}"
+    for j in range(k):
+        want = torch.where(c["label"] == j, c["data"][j], torch.zeros_like(c["data"][j]))
+        assert torch.equal(out[j], want), f"rebuilt shard {j}"

@@ -838,6 +838,21 @@ def test_forced_split_shift(gpu, oracle, shift):
     assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("env,expect", [({"CEC_STORE_POLICY": "nt"}, "nt:%d" % (512 << 20)),
+                                        ({"CEC_STORE_POLICY": "wt"}, "wt:%d" % (512 << 20)),
+                                        ({"CEC_WT_MAX_BYTES": "0"}, "auto:0")])
+def test_store_policy_every_kernel_kind(gpu, oracle, env, expect):
+    """Both store paths of every kernel kind are bit-exact: under the default
+    policy the suite's small launches all take write-through stores, so the non-temporal
+    path is forced here (CEC_STORE_POLICY=nt, and auto with a 0-byte write-through limit),
+    and write-through pinned too.  Child process: the library reads the policy once."""
+    e = {x: v for x, v in os.environ.items() if x not in ("CEC_STORE_POLICY", "CEC_WT_MAX_BYTES")}
+    e.update(env, CEC_EXPECT_POLICY=expect)
+    r = subprocess.run(["python", os.path.join(ROOT, "tests", "split_case.py")], env=e,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip().endswith("OK"), r.stdout[-2000:] + r.stderr[-2000:]
+
+
 def test_pinned_host_arenas_zero_copy(gpu, oracle):
     """bench.py --e2e-zero-copy: pinned host buffers used as arenas by the batched ops
     (the kernels read and write them over PCIe); encode, then a decode of every mask
@@ -978,6 +993,18 @@ def test_bench_two_ranks_one_card_weak_and_strong(gpu):
     st = out["strong"]
     assert st["n_gpus"] == 2 and st["stripes_per_gpu"] == 32768 and st["verified"] is True
     assert st["value"] > 0
+    # the per-rank evidence: both ranks on one card, so the line must NOT pass for a
+    # 2-GPU run; each rank's own step times and identity are carried
+    rk = out["ranks"]
+    assert rk["world_size"] == 2 and rk["backend"] == "gloo" and rk["distinct_devices"] is False
+    ids = [e["identity"] for e in rk["per_rank"]]
+    assert ids[0]["uuid"] == ids[1]["uuid"] and ids[0]["pci"] == ids[1]["pci"] and ids[0]["arch"] == "gfx950"
+    for e in rk["per_rank"]:
+        assert e["weak"]["ms_per_step"] > 0 and e["weak"]["encode_ms"] > 0 and e["weak"]["decode_ms"] > 0
+        assert e["strong"]["ms_per_step"] > 0 and e["strong"]["verified"] is True
+    assert [e["strong"]["stripes"] for e in rk["per_rank"]] == [[0, 32768], [32768, 65536]]
+    assert max(e["weak"]["ms_per_step"] for e in rk["per_rank"]) == pytest.approx(out["ms_per_step"], rel=1e-3)
+    assert rk["slowest_rank_weak"] in (0, 1) and rk["slowest_rank_strong"] in (0, 1)
 
 
 def test_graph_capture_replay(gpu, oracle):

@@ -401,3 +401,122 @@ def test_engine_switch_under_concurrent_ops(gpu, oracle):
         t.join()
         ec.set_engine(default)
     assert flips[0] > 150
+
+
+def test_auto_engine_choices(gpu):
+    """AUTO's per-op rule (cocytus_ec.h), read back from the library itself
+    (cec_last_engine, what bench.py reports): LDS only for cec_decode with one mask for
+    the batch or values of 64 KiB and more; PERM for the 4 KiB encode and rotating decode
+    (the metric), every encode, the diff-update, residual, solve, set diff, apply and
+    region multiply.  A pinned engine is what every op then reports."""
+    torch, ec = gpu
+    P, L = ec.CEC_ENGINE_PERM, ec.CEC_ENGINE_LDS
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    masks = [ec.recovery_mask(k, m, k + p, [int(i != j) for i in range(k + m)])
+             for p in range(m) for j in range(k)]
+    import bench
+
+    mixed = bench.layout("rs32_mixed")[0][:400]
+    base = mixed[0][0]
+    mixed = [(o - base, ln) for o, ln in mixed]
+    size = max(4096 * 64, 65536 * 8, mixed[-1][0] + mixed[-1][1])
+    ar = ec.arena_tensors(2 * k + m + 2, size)
+    data, par, out, stage, res = ar[:k], ar[k:k + m], ar[k + m:2 * k + m], ar[-2], ar[-1]
+    for t in ar:
+        t.random_(0, 256)
+    plans = {"4k": [(s * 4096, 0, 4096) for s in range(64)], "64k": [(s * 65536, 0, 65536) for s in range(8)],
+             "mixed": [(o, 0, ln) for o, ln in mixed]}
+    assert sum(ln for _, ln in mixed) >= (64 << 10) * len(mixed)  # the mixed batch's mean is >= 64 KiB
+
+    def ran(fn):
+        fn()
+        return ec.last_engine()
+
+    def choices():
+        got = {}
+        for name, ext in plans.items():
+            with ec.Plan([(o, s, n, 0) for o, s, n in ext]) as one, \
+                 ec.Plan([(o, s, n, q % 6) for q, (o, s, n) in enumerate(ext)]) as rot:
+                got[f"encode_{name}"] = ran(lambda: ec.encode(k, m, mat, data, par, one))
+                got[f"decode_rotating_{name}"] = ran(lambda: ec.decode(k, m, mat, masks, data + par, out, rot))
+                got[f"decode_one_mask_{name}"] = ran(lambda: ec.decode(k, m, mat, [masks[4]], data + par, out, one))
+        with ec.Plan([(s * 4096, s * 4096, 4096, s % k) for s in range(64)]) as byj, \
+             ec.Plan([(s * 4096, 0, 4096, 0) for s in range(64)]) as one:
+            got["diff_update"] = ran(lambda: ec.diff_update(k, m, mat, data, stage, par, True, byj))
+            got["set_diff"] = ran(lambda: ec.set_diff(k, data, stage, res, byj))
+            got["apply_diffs"] = ran(lambda: ec.apply_diffs(k, m, mat, k + 1, res, par[1], byj))
+            got["residual"] = ran(lambda: ec.residual(k, m, mat, k, masks[0], data + par, res, one))
+            got["solve"] = ran(lambda: ec.solve(k, m, mat, masks[4], [None] * (k + 1) + [res], out, one))
+        got["encode_region"] = ran(lambda: ec.encode_region(k, m, mat, data, par, 65536 * 8))
+        got["region_multiply"] = ran(lambda: ec.region_multiply(data[0], 245, 65536, par[0], 1))
+        torch.cuda.synchronize()
+        return got
+
+    default = ec.get_engine()
+    try:
+        ec.set_engine(ec.CEC_ENGINE_AUTO)
+        got = choices()
+        lds = {"decode_one_mask_4k", "decode_one_mask_64k", "decode_one_mask_mixed", "decode_rotating_64k",
+               "decode_rotating_mixed"}
+        assert got == {op: (L if op in lds else P) for op in got}, got
+        for pinned in (P, L):
+            ec.set_engine(pinned)
+            assert set(choices().values()) == {pinned}
+    finally:
+        ec.set_engine(default)
+
+
+def _c_stream(ec):
+    import ctypes
+
+    s = ctypes.c_void_p()
+    assert ec.lib().cec_stream_create(ctypes.byref(s)) == ec.CEC_OK
+    return s.value
+
+
+def test_release_stream_keeps_tracking_bounded(gpu, oracle):
+    """A long-lived plan, drainer and recovery pool used on 40 short-lived streams (one per
+    client connection), each released (cec_*_release_stream) and then destroyed: the plan
+    tracks no dead stream (its list stays at the streams alive), every result is
+    bit-exact, and the objects' destroys touch no destroyed handle."""
+    torch, ec = gpu
+    k, m, mat, data, parity = _rs32(torch, ec, B=64)
+    torch.cuda.synchronize()
+    plan = ec.Plan([(i * 4096, 0, 4096, 0) for i in range(64)])
+    torch.cuda.synchronize()
+    base = plan.tracked_streams  # the creation stream
+    host = [d.cpu().numpy() for d in data]
+    exp = oracle.encode(mat, k, m, host)
+    n = 64 * 4096
+    drained = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    diff = oracle.splitmix_bytes(77, 4096)
+    want = np.zeros(n, np.uint8)
+    pool_parity = parity[0].clone()
+    with ec.Drainer(k, m, mat, k + 1, staging_bytes=1 << 20) as dr, \
+         ec.RecoveryPool(k, m, mat, k, pool_parity, capacity_units=8) as pool:
+        for i in range(40):
+            s = _c_stream(ec)
+            par = [torch.zeros(n, dtype=torch.uint8, device="cuda") for _ in range(m)]
+            torch.cuda.synchronize()
+            ec.encode(k, m, mat, data, par, plan, s)
+            dr.apply([(diff, (i % 64) * 4096, i % k)], drained, s)
+            oracle.region_multiply(diff.copy(), mat[(k + 1) * k + i % k], want[(i % 64) * 4096:(i % 64 + 1) * 4096], 1)
+            rid = pool.begin(ec.recovery_mask(k, m, k, [0, 1, 1, 1, 1]), i % 64, i % 64)
+            pool.add_peer(rid, 1, host[1][(i % 64) * 4096:(i % 64 + 1) * 4096].copy())
+            pool.flush(s)
+            pool.end(rid)
+            for obj in (plan, dr, pool):
+                obj.release_stream(s)
+            assert plan.tracked_streams == base
+            assert ec.lib().cec_stream_destroy(ctypes_vp(s)) == ec.CEC_OK
+            assert all(np.array_equal(par[p].cpu().numpy(), exp[p]) for p in range(m)), i
+        assert np.array_equal(drained.cpu().numpy(), want)
+    plan.release_stream(12345)  # a stream it never used: no-op
+    plan.destroy()
+
+
+def ctypes_vp(x):
+    import ctypes
+
+    return ctypes.c_void_p(x)

@@ -113,7 +113,12 @@ def main(out, rnd, engine="perm"):
     os.makedirs(prof, exist_ok=True)
     with open(os.path.join(prof, f"{rnd}_pmc_summary.json"), "w") as f:
         json.dump(summary, f, indent=1)
-    # bench.py's `traffic` per engine: pmc_traffic.json (PERM), pmc_traffic_lds.json
+    # bench.py's `traffic` per engine: pmc_traffic.json (PERM), pmc_traffic_lds.json.
+    # `_build` ties the bytes to the kernels they measured: bench.py reports them only
+    # while the library it loads has the same device code (traffic_stale otherwise).
+    from cocytus_amd import ec
+
+    traffic["_build"] = {"kernel_code_id": ec.kernel_code_id(), "round": rnd, "engine": engine}
     with open(os.path.join(prof, "pmc_traffic.json" if engine == "perm" else f"pmc_traffic_{engine}.json"),
               "w") as f:
         json.dump(traffic, f, indent=1)
