@@ -1,0 +1,35 @@
+#!/bin/bash
+# Round-4 gpurun calls, one case per call: `gpurun -- bash tools/r04_calls.sh <letter>`.
+# Each GPU step runs under its own timeout; a step that faults, aborts or times out
+# ends the call (rc > 1; pytest's rc 1 = failed tests, which the call reports and goes on).
+# The letter names the gpurun_out/r04<letter>/ directory the call wrote, whose kept files
+# are under profiles/r04_evidence/.
+call=$1
+mkdir -p gpurun_out/r04$call
+run() { name=$1; shift; timeout -k 10 "$@" > gpurun_out/r04$call/$name.log 2>&1; rc=$?; echo "$name rc=$rc"; if [ $rc -gt 1 ]; then exit $rc; fi; }
+PYT="python -u -m pytest -v --timeout 300 --timeout-method thread"
+case "$call" in
+a)
+  # this round's new GPU tests first (configs[2] at full size, AUTO's choices, released
+  # streams, both store policies on every kernel kind, the 2-rank line's evidence), then
+  # the whole GPU suite, then the default bench line
+  run new_tests 900 $PYT -m gpu tests/test_gpu_golden.py::test_cfg3_mixed_full_size \
+      tests/test_gpu_runtime.py::test_auto_engine_choices tests/test_gpu_runtime.py::test_release_stream_keeps_tracking_bounded \
+      tests/test_gpu_parity.py::test_store_policy_every_kernel_kind tests/test_gpu_parity.py::test_bench_two_ranks_one_card_weak_and_strong
+  run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  run bench_default 300 python -u bench.py
+  ;;
+b)
+  # every DESIGN §5 number from one box (no profiles: call c)
+  EVID_NO_PROF=1 timeout -k 10 1100 bash tools/round_evidence.sh r04
+  ;;
+c)
+  # rocprofv3 on this round's kernels: kernel-trace stats and the FETCH_SIZE / WRITE_SIZE
+  # passes per workload, PERM (profiles/pmc_traffic.json) and LDS (pmc_traffic_lds.json,
+  # the workloads whose decode AUTO runs with it), each summary stamped with the kernels'
+  # code id (bench.py reports traffic only for the kernels it measured)
+  timeout -k 10 560 bash tools/profile_round.sh r04 > gpurun_out/r04c/profile.log 2>&1 && \
+  PROF_ENGINE=lds PROF_WORKLOADS="rs32_4k rs32_mixed rs42_64k rs32_1m rs32_diff_update" \
+      timeout -k 10 560 bash tools/profile_round.sh r04_lds > gpurun_out/r04c/profile_lds.log 2>&1
+  ;;
+esac
