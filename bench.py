@@ -160,11 +160,18 @@ def shard_stripes(stripes, rank: int, world: int) -> tuple[int, int]:
     return (cut(rank), cut(rank + 1) if rank + 1 < world else len(stripes))
 
 
+def dist_on(dist) -> bool:
+    """A process group is up (world size > 1, or CEC_BENCH_PG=1 at world size 1): the
+    barriers and the max over ranks then run as collectives."""
+    return dist is not None and dist.is_available() and dist.is_initialized()
+
+
 def max_over_ranks(values, dist):
-    """Element-wise max of a list of floats over all ranks (identity when alone)."""
+    """Element-wise max of a list of floats over all ranks (identity without a process
+    group; a real all_reduce with one, even of one rank)."""
     import torch
 
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist_on(dist):
         return [float(x) for x in values]
     device = "cuda" if dist.get_backend() == "nccl" else "cpu"
     t = torch.tensor(values, dtype=torch.float64, device=device)
@@ -321,7 +328,7 @@ def device_identity(torch, dev) -> dict:
 def gather_ranks(dist, mine: dict) -> list:
     """Every rank's entry, in rank order, on every rank (one all_gather_object, outside
     every timed region; identity when alone)."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist_on(dist):
         return [mine]
     out = [None] * dist.get_world_size()
     dist.all_gather_object(out, mine)
@@ -353,7 +360,14 @@ def setup(backend="nccl"):
     # multi-rank path on a one-GPU box (never used for reported numbers).
     dev = int(os.environ.get("CEC_BENCH_DEVICE", local))
     torch.cuda.set_device(dev)
-    if world > 1:
+    # CEC_BENCH_PG=1 brings the process group up at world size 1 as well (a one-rank RCCL
+    # communicator): the N > 1 line's collectives -- barriers, the all_reduce MAX, the
+    # per-rank all_gather -- then run on a one-GPU box (tests/test_gpu_parity.py).
+    if world > 1 or os.environ.get("CEC_BENCH_PG") == "1":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -448,7 +462,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     evs = [ec.Event() for _ in range(2 * args.steps + 1)]
     host = [0.0, 0.0]  # host time spent enqueueing the encodes / the decodes
     pc = time.perf_counter
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = pc()
@@ -467,7 +481,7 @@ def measure_device(torch, dist, ec, world, rank, workload, args, share=None):
     t_enq = pc() - t0  # the host is this far ahead of the GPU when the loop ends
     torch.cuda.synchronize()
     elapsed = pc() - t0  # this rank's K steps; the max over ranks is taken below
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     own_elapsed = elapsed
     enc_t = [evs[2 * s].elapsed_ms(evs[2 * s + 1]) for s in range(args.steps)]
@@ -606,7 +620,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
     eng = engine_ran(ec)  # the library's own report of the engine the op ran with
     evs = [ec.Event() for _ in range(args.steps + 1)]
     torch.cuda.synchronize()
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -616,7 +630,7 @@ def measure_diff_update(torch, dist, ec, world, rank, args):
         evs[s + 1].record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     du_t = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
     ms = sum(du_t) / args.steps
@@ -676,7 +690,7 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
         eng = engine_ran(ec)
         evs = [ec.Event() for _ in range(args.steps + 1)]
         torch.cuda.synchronize()
-        if world > 1:
+        if dist_on(dist):
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -686,7 +700,7 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
             evs[s + 1].record(stream)
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
-        if world > 1:
+        if dist_on(dist):
             dist.barrier()
         ts = [evs[s].elapsed_ms(evs[s + 1]) for s in range(args.steps)]
         ms = sum(ts) / args.steps
@@ -803,7 +817,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
     torch.cuda.synchronize()
     ok = e.verified()
     steps = max(1, min(args.steps, 10))
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -811,7 +825,7 @@ def measure_e2e(torch, dist, ec, world, rank, args):
         e.step()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     h2d, d2h = pcie_raw(torch)
     floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
@@ -884,11 +898,10 @@ def run_device(args):
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
             "identity": device_identity(torch, torch.cuda.current_device()),
             "weak": r["rank"], "strong": strong.pop("rank", None) if strong else None,
-            "other_workloads": {w: v.pop("rank", None) for w, v in also.items()}}
-    for v in also.values():  # the recovery cases carry theirs per case
-        for c in v.get("cases", {}).values():
-            c.pop("rank", None)
-    ranks = ranks_summary(gather_ranks(dist, mine), dist.get_backend() if world > 1 else "none")
+            "other_workloads": {w: v.pop("rank", None) or  # the recovery cases carry theirs per case
+                                {n: c.pop("rank", None) for n, c in v.get("cases", {}).items()}
+                                for w, v in also.items()}}
+    ranks = ranks_summary(gather_ranks(dist, mine), dist.get_backend() if dist_on(dist) else "none")
     if rank == 0:
         k, m, n, B = r["k"], r["m"], r["n"], r["B"]
         res = {
@@ -1282,20 +1295,24 @@ def run_harness_check(args):
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if world > 1:
+    if world > 1 or os.environ.get("CEC_BENCH_PG") == "1":
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(free_port()))
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         dist.init_process_group("gloo")
     lo, hi = shard_range(WORKLOADS["rs32_4k"][3] * world, rank, world)
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     t0 = time.perf_counter()
     time.sleep(0.01 * (rank + 1))  # ranks finish at different times: the max must win
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if dist_on(dist):
         dist.barrier()
     mine = [float(elapsed), float(0.01 * (rank + 1)), float(rank)]
-    got = max_over_ranks(mine, dist if world > 1 else None)
+    got = max_over_ranks(mine, dist)
     spans = [None] * world
-    if world > 1:
+    if dist_on(dist):
         dist.all_gather_object(spans, (rank, lo, hi))
     else:
         spans = [(0, lo, hi)]
@@ -1307,7 +1324,7 @@ def run_harness_check(args):
              "pci": None, "uuid": f"cpu-{shared}" if shared else f"cpu-{os.getpid()}"}
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")), "identity": ident,
             "weak": {"ms_per_step": round(elapsed * 1e3, 4), "stripes": [lo, hi]}, "strong": None}
-    ranks = ranks_summary(gather_ranks(dist if world > 1 else None, mine), "gloo" if world > 1 else "none")
+    ranks = ranks_summary(gather_ranks(dist, mine), dist.get_backend() if dist_on(dist) else "none")
     if rank == 0:
         print(json.dumps({"harness_check": True, "n_gpus": world, "gpus_arg": args.gpus,
                           "elapsed_max": got[0], "slowest_sleep": got[1], "max_rank": got[2],

@@ -149,6 +149,19 @@ def test_bench_single_rank_runs_in_process():
     assert out["n_gpus"] == 1 and out["shards"] == [[0, 0, 65536]]
 
 
+def test_bench_process_group_at_world_one():
+    """CEC_BENCH_PG=1: the process group comes up at world size 1 too, so the line's
+    collectives (barrier, all_reduce MAX, all_gather of the per-rank evidence) run as
+    real collectives on a one-device box (the GPU twin runs a one-rank RCCL group)."""
+    import json
+
+    r = _run_bench(["--harness-check"], env_extra={"CEC_BENCH_PG": "1"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["ranks"]["backend"] == "gloo" and out["ranks"]["world_size"] == 1
+    assert out["shards"] == [[0, 0, 65536]]
+
+
 def test_bench_world_size_mismatch_refused():
     r = _run_bench(["--gpus", "2", "--harness-check"],
                    env_extra={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"}, timeout=120)

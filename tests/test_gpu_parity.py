@@ -1007,6 +1007,30 @@ def test_bench_two_ranks_one_card_weak_and_strong(gpu):
     assert rk["slowest_rank_weak"] in (0, 1) and rk["slowest_rank_strong"] in (0, 1)
 
 
+def test_bench_rccl_path_one_rank(gpu):
+    """The N > 1 line's RCCL path on this one card: CEC_BENCH_PG=1 brings up a one-rank
+    nccl (= RCCL) process group with the device bound (init_process_group(device_id=)),
+    so the barriers, the all_reduce MAX over ranks and the all_gather of the per-rank
+    evidence all run through RCCL as they do for the driver's N-GPU run (two ranks on one
+    card is refused by RCCL, hence one)."""
+    import json
+
+    env = {x: v for x, v in os.environ.items()
+           if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT", "CEC_BENCH_DEVICE")}
+    env["CEC_BENCH_PG"] = "1"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "3", "--warmup", "1",
+                        "--also=rs32_diff_update,rs32_1m_recovery", "--no-cpu-baseline", "--dist-backend", "nccl"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["verified"] is True
+    rk = out["ranks"]
+    assert rk["backend"] == "nccl" and rk["world_size"] == 1 and rk["distinct_devices"] is True
+    e = rk["per_rank"][0]
+    assert e["identity"]["arch"] == "gfx950" and e["weak"]["ms_per_step"] == pytest.approx(out["ms_per_step"], rel=1e-3)
+    assert set(e["other_workloads"]) == {"rs32_diff_update", "rs32_1m_recovery"}
+
+
 def test_graph_capture_replay(gpu, oracle):
     """An encode + decode step captured into a HIP graph (torch.cuda.graph) replays
     bit-exactly; the coefficient tables are cached by a warm-up call before capture."""
