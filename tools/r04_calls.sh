@@ -32,4 +32,10 @@ c)
   PROF_ENGINE=lds PROF_WORKLOADS="rs32_4k rs32_mixed rs42_64k rs32_1m rs32_diff_update" \
       timeout -k 10 560 bash tools/profile_round.sh r04_lds > gpurun_out/r04c/profile_lds.log 2>&1
   ;;
+d)
+  # the one-rank RCCL path of the N > 1 line, the 2-rank one-card line, then the suite
+  run rccl_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_bench_rccl_path_one_rank \
+      tests/test_gpu_parity.py::test_bench_two_ranks_one_card_weak_and_strong
+  run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  ;;
 esac
