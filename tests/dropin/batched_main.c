@@ -11,6 +11,9 @@
  *   4. D0 lost, leader P0: single-unit recovery requests through a cec_recovery_pool,
  *      replies from host copies of D1..D(K-1), half received in place, rebuilt by
  *      cec_recovery_pool_flush_solve into an out arena
+ * The drain and every window of the pool run on a short-lived stream of their own (a
+ * connection's), released from the long-lived object before it is destroyed
+ * (cec_*_release_stream, the LIFETIME RULE of cocytus_ec.h).
  * Input  (argv[1]): int32 K, M, units, nsets; nsets x int32 (lid, addr, len); the K data
  *        arenas (units x 4096 B each); the SETs' new values back to back.
  * Output (argv[2]): the M parity arenas, the K data arenas after install, the drained
@@ -114,7 +117,11 @@ int main(int argc, char **argv) {
     /* 3. the parity side: drain every diff into the copy of parity K+1 */
     cec_drainer *dr;
     CE(cec_drainer_create(&dr, K, M, matrix, K + 1, 1 << 20));
-    CE(cec_drainer_apply(dr, ups, nsets, drained, NULL));
+    void *conn;
+    CE(cec_stream_create(&conn));
+    CE(cec_drainer_apply(dr, ups, nsets, drained, conn));
+    CE(cec_drainer_release_stream(dr, conn));
+    CE(cec_stream_destroy(conn));
     CE(cec_drainer_destroy(dr));
 
     /* 4. D0 lost, leader P0: one request per unit through a pool, replies from host
@@ -148,8 +155,11 @@ int main(int argc, char **argv) {
                 }
             }
         }
-        const int solved = cec_recovery_pool_flush_solve(pool, outs, NULL);
+        CE(cec_stream_create(&conn));
+        const int solved = cec_recovery_pool_flush_solve(pool, outs, conn);
         CE(solved);
+        CE(cec_recovery_pool_release_stream(pool, conn));
+        CE(cec_stream_destroy(conn));
         if (solved != w) {
             fprintf(stderr, "solved %d of %d\n", solved, w);
             return 4;

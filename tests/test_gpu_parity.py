@@ -1007,6 +1007,32 @@ def test_bench_two_ranks_one_card_weak_and_strong(gpu):
     assert rk["slowest_rank_weak"] in (0, 1) and rk["slowest_rank_strong"] in (0, 1)
 
 
+def test_cfg4_eight_rank_batches_one_card(gpu):
+    """BASELINE configs[3] ("RS(4,2) parity encode, 64 KiB values, 8 x MI355X, independent
+    batches sharded per GPU") through the driver's multi-GPU entry point with its 8 ranks
+    on this one card (gloo, CEC_BENCH_DEVICE=0): each rank encodes its own 16,384-stripe
+    batch (seeded per rank) and rebuilds a rotating lost shard of every stripe, checked
+    byte for byte on the device; the line reports all 8 ranks verified, n_gpus 8, and,
+    correctly, distinct_devices false.  (The rates are not scaling numbers: the ranks
+    share one card.)"""
+    import json
+
+    env = {x: v for x, v in os.environ.items()
+           if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env["CEC_BENCH_DEVICE"] = "0"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--workload", "rs42_64k",
+                        "--steps", "2", "--warmup", "1", "--also=", "--no-strong", "--no-cpu-baseline"],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert out["n_gpus"] == 8 and out["verified"] is True
+    assert out["config"]["k"] == 4 and out["config"]["m"] == 2 and out["config"]["stripes_per_gpu"] == 16384
+    rk = out["ranks"]
+    assert rk["world_size"] == 8 and rk["distinct_devices"] is False
+    assert [e["rank"] for e in rk["per_rank"]] == list(range(8))
+    assert all(e["weak"]["verified"] for e in rk["per_rank"])
+
+
 def test_bench_rccl_path_one_rank(gpu):
     """The N > 1 line's RCCL path on this one card: CEC_BENCH_PG=1 brings up a one-rank
     nccl (= RCCL) process group with the device bound (init_process_group(device_id=)),

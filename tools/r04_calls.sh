@@ -35,7 +35,14 @@ c)
 d)
   # the one-rank RCCL path of the N > 1 line, the 2-rank one-card line, then the suite
   run rccl_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_bench_rccl_path_one_rank \
-      tests/test_gpu_parity.py::test_bench_two_ranks_one_card_weak_and_strong
+      tests/test_gpu_parity.py::test_bench_two_ranks_one_card_weak_and_strong \
+      tests/test_gpu_parity.py::test_cfg4_eight_rank_batches_one_card
   run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  # host code under ASan + UBSan and TSan (built here: tools/asan.sh build, tools/tsan.sh
+  # build; .gpurunignore lets tools/asan and tools/tsan travel for this call only)
+  if [ -f tools/asan/libcocytus_ec.so ] && [ -f tools/tsan/libcocytus_ec.so ]; then
+    run asan 600 bash tools/asan.sh run
+    run tsan 600 bash tools/tsan.sh run
+  fi
   ;;
 esac

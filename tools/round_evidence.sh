@@ -37,6 +37,12 @@ CEC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 2 > "$OUT/bench_gloo
 # the driver's N: 8 ranks on one card (gloo), the weak line and the fixed-batch split
 CEC_BENCH_WATCHDOG=60 CEC_BENCH_DEVICE=0 timeout -k 10 500 python bench.py --gpus 8 --also= \
     > "$OUT/bench_gloo8_one_card.jsonl" 2> "$OUT/bench_gloo8.err"
+# configs[3] as stated (RS(4,2) 64 KiB, 8 independent rank batches), its 8 ranks on one card
+CEC_BENCH_DEVICE=0 timeout -k 10 400 python bench.py --gpus 8 --workload rs42_64k --also= --no-strong \
+    --no-cpu-baseline > "$OUT/bench_gloo8_rs42_one_card.jsonl" 2> "$OUT/bench_gloo8_rs42.err"
+# the N > 1 line's RCCL collectives on a one-rank communicator
+CEC_BENCH_PG=1 timeout -k 10 300 python bench.py --dist-backend nccl --no-cpu-baseline \
+    > "$OUT/bench_rccl_one_rank.jsonl" 2> "$OUT/bench_rccl_one_rank.err"
 timeout -k 10 120 tools/xcd_visibility_probe.bin 64 200 > "$OUT/xcd_visibility.jsonl" 2>&1
 timeout -k 10 120 tools/small_batch_probe.bin 20 > "$OUT/small_batch_probe.jsonl" 2>&1
 timeout -k 10 200 python tools/du_probe.py > "$OUT/du_probe.json" 2>/dev/null
