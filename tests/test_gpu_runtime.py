@@ -520,3 +520,32 @@ def ctypes_vp(x):
     import ctypes
 
     return ctypes.c_void_p(x)
+
+
+def test_release_stream_refused_while_capturing(gpu, oracle):
+    """cec_plan_release_stream on a stream that is being captured into a graph cannot wait
+    for it: refused (CEC_EHIP), the plan keeps the stream listed and the capture is
+    unharmed; after the capture the release works."""
+    torch, ec = gpu
+    k, m, mat, data, parity = _rs32(torch, ec, B=16)
+    s = torch.cuda.Stream()
+    plan = ec.Plan([(i * 4096, 0, 4096, 0) for i in range(16)], stream=s)
+    ec.encode(k, m, mat, data, parity, plan, s)  # tables cached, s listed
+    s.synchronize()
+    listed = plan.tracked_streams
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        with pytest.raises(ec.CecError) as ei:
+            plan.release_stream(s)
+        assert ei.value.code == ec.CEC_EHIP
+        ec.encode(k, m, mat, data, parity, plan, s)
+    assert plan.tracked_streams == listed
+    for p in parity:
+        p.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    exp = oracle.encode(mat, k, m, [d.cpu().numpy() for d in data])
+    assert all(np.array_equal(parity[p].cpu().numpy(), exp[p]) for p in range(m))
+    plan.release_stream(s)
+    assert plan.tracked_streams == listed - 1
+    plan.destroy()

@@ -48,7 +48,7 @@ d)
 e)
   # whole-batch oracle parity for configs[3] and configs[4], then the suite
   run cfg_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_cfg4_rs42_64k_roundtrip \
-      tests/test_gpu_parity.py::test_cfg5_1mib_decode_d0_p0_and_d1_p1
+      tests/test_gpu_parity.py::test_cfg5_1mib_decode_d0_p0_and_d1_p1 tests/test_gpu_runtime.py::test_release_stream_refused_while_capturing
   run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   ;;
 esac
