@@ -76,8 +76,8 @@ def parse(argv=None):
     ap.add_argument("--workload", default="rs32_4k", choices=sorted(WORKLOADS))
     ap.add_argument("--engine", default="auto", choices=["auto", "perm", "lds"],
                     help="GF(2^8) engine (cec_set_engine); auto = the library default: LDS for "
-                         "single-mask decodes and decodes of values of 64 KiB and more, PERM for "
-                         "every other op (cocytus_ec.h)")
+                         "decodes of values of 64 KiB and more, PERM for every other op "
+                         "(cocytus_ec.h)")
     ap.add_argument("--e2e", action="store_true", help="pinned host -> HBM -> host pipeline")
     ap.add_argument("--e2e-streams", type=int, default=6)  # best of a 3..16 sweep
     ap.add_argument("--drain", action="store_true", help="batched parity drain from host diffs")
@@ -925,8 +925,8 @@ def run_device(args):
                 "parallelism": f"{world} x independent stripe batches, no collective",
                 "engine": (args.engine if args.engine != "auto" else "auto") +
                           f" (ran: encode {r['engine']['encode'].upper()}, decode {r['engine']['decode'].upper()}, "
-                          "as cec_last_engine reports; AUTO = LDS for single-mask decodes and decodes of "
-                          "values of 64 KiB and more, PERM for every other op)",
+                          "as cec_last_engine reports; AUTO = LDS for decodes of values of 64 KiB and more, "
+                          "PERM for every other op)",
             },
             "roofline": r["roofline"],
             "decode_roofline": r["decode_roofline"],

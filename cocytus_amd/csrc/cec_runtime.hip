@@ -75,10 +75,9 @@ static std::atomic<int> g_engine{CEC_ENGINE_AUTO};
 
 // The engine an op runs with, read once per op (its tables and its kernel must agree):
 // the process-wide setting, or under AUTO the LDS engine only where it led PERM by more
-// than 2 % on the median of the recorded boxes -- `lds_op`: a decode with one mask for
-// the whole batch, or of values of 64 KiB and more -- and PERM for every other op
-// (cocytus_ec.h; DESIGN.md §4 "Engine per op").  Recorded per thread for
-// cec_last_engine().
+// than 2 % on the median of the recorded boxes -- `lds_op`: a decode of values of 64 KiB
+// and more -- and PERM for every other op (cocytus_ec.h; DESIGN.md §4 "Engine per op").
+// Recorded per thread for cec_last_engine().
 static thread_local int t_last_engine = -1;
 static int op_engine(bool lds_op) {
     const int e = g_engine.load();
@@ -1157,13 +1156,11 @@ CEC_API int cec_decode(int k, int m, const int *matrix, const uint32_t *masks, i
             c.outs.push_back(o);
         }
     }
-    // AUTO: one recovery mask for the whole batch (a server rebuilding one lid) runs the
-    // LDS engine (2.2-4.8 % ahead of PERM with a non-unit leader inverse,
-    // profiles/r03_evidence/engine_auto/), and so do large values (large_values);
-    // erasures that vary per 4 KiB value run PERM (ahead by 2-3 % on the bench's
-    // rotating masks)
+    // AUTO: values of 64 KiB and more (large_values) run the LDS engine, ahead of PERM by a
+    // median 3 % there (rotating or one mask: configs[4]'s 1 MiB D1-by-P1 rebuild +4.9 %);
+    // 4 KiB values run PERM (rotating masks -1.7 %, one mask +1.1 %: within 2 %)
     return run_combos(dev, st, combos, plan, 0, static_cast<hipStream_t>(stream), nullptr,
-                      n_masks == 1 || large_values(plan));
+                      large_values(plan));
 }
 
 CEC_API uint32_t cec_recovery_mask(int k, int m, int leader_lid, const int *connected) {

@@ -29,7 +29,7 @@ CEC_ENODEV = -6
 CEC_EFULL = -7
 CEC_ENGINE_PERM = 0
 CEC_ENGINE_LDS = 1
-CEC_ENGINE_AUTO = 2  # default: LDS for single-mask and large-value decodes, PERM for the rest (cocytus_ec.h)
+CEC_ENGINE_AUTO = 2  # default: LDS for decodes of values >= 64 KiB, PERM for the rest (cocytus_ec.h)
 CEC_MAX_K = 16
 CEC_MAX_M = 8
 UNIT_SIZE = 4096

@@ -91,11 +91,10 @@ typedef struct cec_plan cec_plan;
  * (pure VALU, no LDS); LDS stages one 256-entry product row per coefficient,
  * exp[log x + log c] built from the log / antilog tables, in LDS (one ds_read_u8 per
  * byte).  AUTO (default) runs the LDS engine only where it led PERM by more than 2 % on
- * the median of the recorded boxes: cec_decode with one mask for the
- * whole batch (n_masks == 1), or of values of 64 KiB and more (the plan's mean extent).
- * Every other op runs PERM: encodes (any size), per-value rotating decodes of smaller
- * values, the diff-update, residual, solve, set diff, apply, region multiply and the
- * recovery sessions and pool. */
+ * the median of the recorded boxes: cec_decode of values of 64 KiB and
+ * more (the plan's mean extent), with one mask or many.  Every other op runs PERM:
+ * encodes (any size), decodes of smaller values, the diff-update, residual, solve, set
+ * diff, apply, region multiply and the recovery sessions and pool. */
 typedef enum cec_engine { CEC_ENGINE_PERM = 0, CEC_ENGINE_LDS = 1, CEC_ENGINE_AUTO = 2 } cec_engine;
 
 /* ---- runtime ---- */

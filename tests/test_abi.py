@@ -150,8 +150,8 @@ def test_arena_stride_is_odd_pages(lib):
 
 def test_default_engine_is_auto(lib):
     """The product default is AUTO: the LDS engine only where it led PERM by more than 2 %
-    on the median of the recorded boxes -- cec_decode with one mask for the batch, or of
-    values of 64 KiB and more -- and PERM for every other op (cocytus_ec.h, DESIGN.md §4;
+    on the median of the recorded boxes -- cec_decode of values of 64 KiB and more -- and
+    PERM for every other op (cocytus_ec.h, DESIGN.md §4;
     the choices themselves are asserted on the GPU, test_auto_engine_choices).  PERM and
     LDS stay selectable and both are in every GPU parity test; AUTO is what every test
     that leaves the engine alone runs."""

@@ -405,10 +405,11 @@ def test_engine_switch_under_concurrent_ops(gpu, oracle):
 
 def test_auto_engine_choices(gpu):
     """AUTO's per-op rule (cocytus_ec.h), read back from the library itself
-    (cec_last_engine, what bench.py reports): LDS only for cec_decode with one mask for
-    the batch or values of 64 KiB and more; PERM for the 4 KiB encode and rotating decode
-    (the metric), every encode, the diff-update, residual, solve, set diff, apply and
-    region multiply.  A pinned engine is what every op then reports."""
+    (cec_last_engine, what bench.py reports): LDS only for cec_decode of values of 64 KiB
+    and more (one mask or many); PERM for the 4 KiB encode and rotating decode (the
+    metric), 4 KiB single-mask decodes, every encode, the diff-update, residual, solve,
+    set diff, apply and region multiply.  A pinned engine is what every op then
+    reports."""
     torch, ec = gpu
     P, L = ec.CEC_ENGINE_PERM, ec.CEC_ENGINE_LDS
     k, m = 3, 2
@@ -457,8 +458,7 @@ def test_auto_engine_choices(gpu):
     try:
         ec.set_engine(ec.CEC_ENGINE_AUTO)
         got = choices()
-        lds = {"decode_one_mask_4k", "decode_one_mask_64k", "decode_one_mask_mixed", "decode_rotating_64k",
-               "decode_rotating_mixed"}
+        lds = {"decode_one_mask_64k", "decode_one_mask_mixed", "decode_rotating_64k", "decode_rotating_mixed"}
         assert got == {op: (L if op in lds else P) for op in got}, got
         for pinned in (P, L):
             ec.set_engine(pinned)
