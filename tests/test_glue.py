@@ -1,0 +1,133 @@
+"""The server glue of integration/ (cocytus_drain.c: the parity process's drain loops,
+memcached.c:4231/4322/4350/8068 -> process_rep_command :7739-7798, batched onto one
+cec_drainer_apply) driven over the server's own queue type: oracle/_ref/glue_drain is
+built (oracle/Makefile `ref`) from the glue and tests/glue/drain_main.c against the
+reference's rep_queue.h where it lies.  Skips where it was not built (no /root/reference
+when the tree was built).
+
+CPU: which queued diffs a drain call takes (the xid window, ring order and wrap, the
+item's nbytes rather than the buffer's capacity, a missing xid, more than cap).
+GPU: the parity arena after cocytus_drain_gf equals the reference's sequential loop
+(one region multiply per non-vetoed xid, in xid order) computed by the oracle.
+"""
+from __future__ import annotations
+
+import os
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+EXE = os.path.join(ROOT, "oracle", "_ref", "glue_drain")
+
+
+def _need_exe():
+    if not os.path.exists(EXE):
+        pytest.skip("oracle/_ref/glue_drain not built (make -C oracle ref)")
+
+
+def write_input(path, *, lid, self_lid, k, m, ring, tail, entries, done, stable, cap, arena=0, parity=None):
+    """entries: [(xid, addr, bytes, vnbytes, veto)] at ring indices tail, tail+1, ..."""
+    with open(path, "wb") as f:
+        f.write(struct.pack("<9i", lid, self_lid, k, m, ring, tail, len(entries), arena, cap))
+        f.write(struct.pack("<2Q", done, stable))
+        for xid, addr, val, vn, veto in entries:
+            f.write(struct.pack("<2Q3i", xid, addr, len(val), vn, veto))
+        for _, _, val, _, _ in entries:
+            f.write(bytes(val))
+        if parity is not None:
+            f.write(parity.tobytes())
+
+
+def run(mode, tmp_path, **kw):
+    inp, out = tmp_path / "in.bin", tmp_path / "out.bin"
+    write_input(inp, **kw)
+    r = subprocess.run([EXE, mode, str(inp), str(out)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return r, out
+
+
+def collect(tmp_path, **kw):
+    _, out = run("collect", tmp_path, **kw)
+    lines = out.read_text().split("\n")
+    if lines[0].startswith("rc "):
+        return int(lines[0].split()[1])
+    return [tuple(int(v) for v in ln.split()) for ln in lines if ln]
+
+
+def test_collect_window_ring_and_lengths(tmp_path):
+    """Entries with done_xid < xid <= stable_xid, in xid order, walking the ring [tail,
+    head) across its wrap; len = the item's nbytes, not the buffer's vnbytes (which may be
+    up to twice as large, memcached.c:7727-7731); src_lid = the peer."""
+    _need_exe()
+    rng = np.random.default_rng(3)
+    ents = []
+    for i in range(60):  # xids 101..160, ring of 64 entries starting near its end
+        n = int(rng.integers(1, 300))
+        ents.append((101 + i, 16 * int(rng.integers(0, 1 << 16)), rng.integers(0, 256, n, dtype=np.uint8),
+                     n + int(rng.integers(0, n + 1)), 0))
+    got = collect(tmp_path, lid=2, self_lid=4, k=3, m=2, ring=64, tail=50, entries=ents, done=110,
+                  stable=150, cap=64)
+    want = [(e, ents[e][1], len(ents[e][2]), 2) for e in range(60) if 110 < ents[e][0] <= 150]
+    assert got == want and len(got) == 40
+    # nothing pending: no update
+    assert collect(tmp_path, lid=2, self_lid=4, k=3, m=2, ring=64, tail=50, entries=ents, done=150,
+                   stable=150, cap=64) == []
+
+
+def test_collect_refuses_gaps_and_overflow(tmp_path):
+    """A missing xid of the window is refused (process_rep_command asserts its entry
+    exists), and a window wider than the caller's scratch is CEC_EFULL (drain it in
+    several calls); a repeated xid resolves to its first entry, as rep_queue_find."""
+    _need_exe()
+    v = np.arange(8, dtype=np.uint8)
+    ents = [(x, 16 * x, v, 8, 0) for x in (1, 2, 3, 5, 6)]
+    assert collect(tmp_path, lid=0, self_lid=3, k=3, m=2, ring=8, tail=0, entries=ents, done=0, stable=6,
+                   cap=16) == -1  # CEC_EINVAL: xid 4 missing
+    assert collect(tmp_path, lid=0, self_lid=3, k=3, m=2, ring=8, tail=0, entries=ents, done=0, stable=3,
+                   cap=2) == -7  # CEC_EFULL
+    dup = [(1, 16, v, 8, 0), (2, 32, v, 8, 0), (2, 48, v, 8, 0), (3, 64, v, 8, 0)]
+    got = collect(tmp_path, lid=1, self_lid=3, k=3, m=2, ring=8, tail=6, entries=dup, done=0, stable=3, cap=8)
+    assert [(a, n) for _, a, n, _ in got] == [(16, 8), (32, 8), (64, 8)]
+
+
+@pytest.mark.gpu
+def test_drain_gf_matches_sequential_loop(gpu, oracle, tmp_path):
+    """cocytus_drain_gf over 3,000 queued diffs of one data peer (random lengths 1 B -
+    20 KiB at 16-B-aligned, overlapping addresses of a 4 MiB parity arena; 10 % vetoed by
+    the recovery hook; a window in the middle of the ring, across its wrap) leaves the
+    device parity arena equal to the reference's loop: for each xid in order, if the fold
+    lets it through, parity[addr..] ^= MATRIX(self, lid) * diff (memcached.c:7758-7767),
+    computed by the oracle."""
+    _need_exe()
+    k, m, lid, self_lid = 3, 2, 1, 4
+    arena = 4 << 20
+    rng = np.random.default_rng(11)
+    ents = []
+    for i in range(3000):
+        n = int(rng.integers(1, 20 << 10))
+        addr = 16 * int(rng.integers(0, (arena - n) // 16))
+        ents.append((1000 + i, addr, rng.integers(0, 256, n, dtype=np.uint8), n + int(rng.integers(0, 64)),
+                     int(rng.random() < 0.1)))
+    parity = rng.integers(0, 256, arena, dtype=np.uint8)
+    done, stable = 1000 + 200, 1000 + 2800
+    r, out = run("apply", tmp_path, lid=lid, self_lid=self_lid, k=k, m=m, ring=4096, tail=3000, entries=ents,
+                 done=done, stable=stable, cap=4096, arena=arena, parity=parity)
+    got = np.fromfile(out, dtype=np.uint8)
+    c = oracle.big_vandermonde(k + m, k)[self_lid * k + lid]
+    want = parity.copy()
+    applied = vetoed = 0
+    for xid, addr, val, _, veto in ents:  # already in xid order
+        if not done < xid <= stable:
+            continue
+        if veto:
+            vetoed += 1
+            continue
+        oracle.region_multiply(val.copy(), c, want[addr:addr + len(val)], 1)
+        applied += 1
+    assert np.array_equal(got, want)
+    words = r.stdout.split()
+    assert words[:4] == ["applied", str(applied), "vetoed", str(vetoed)], r.stdout
+    assert int(words[5]) >= 2  # overlapping diffs went to separate waves

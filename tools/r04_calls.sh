@@ -55,7 +55,7 @@ f)
   # AUTO's final rule (LDS only for decodes of values >= 64 KiB), the suite, then the
   # round's canonical evidence set on the final build (no profiles: kernels unchanged)
   run auto_tests 600 $PYT -m gpu tests/test_gpu_runtime.py::test_auto_engine_choices \
-      tests/test_gpu_golden.py::test_cfg3_mixed_full_size
+      tests/test_gpu_golden.py::test_cfg3_mixed_full_size tests/test_glue.py
   run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   EVID_NO_PROF=1 timeout -k 10 900 bash tools/round_evidence.sh r04f
   ;;
