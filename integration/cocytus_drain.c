@@ -18,7 +18,7 @@ int cocytus_drain_collect(const struct rep_queue *q, int lid, uint64_t done_xid,
     if (stable_xid <= done_xid) return 0;
     if (stable_xid - done_xid > (uint64_t)cap) return CEC_EFULL;
     const int n = (int)(stable_xid - done_xid);
-    if (q->cap == 0 || !q->items) return CEC_EINVAL;
+    if (q->cap == 0 || !q->items || q->head - q->tail > q->cap) return CEC_EINVAL; /* not a queue */
     char *seen = calloc((size_t)n, 1);
     if (!seen) return CEC_ENOMEM;
     /* rep_queue_find's walk: tail .. head in ring order; the first entry of an xid wins */
