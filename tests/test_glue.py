@@ -131,3 +131,26 @@ def test_drain_gf_matches_sequential_loop(gpu, oracle, tmp_path):
     words = r.stdout.split()
     assert words[:4] == ["applied", str(applied), "vetoed", str(vetoed)], r.stdout
     assert int(words[5]) >= 2  # overlapping diffs went to separate waves
+
+
+def test_collect_under_asan_ubsan(tmp_path):
+    """The glue's host walk of the ring under AddressSanitizer + UBSan (gcc), over the
+    same cases as above: no out-of-bounds access, no undefined behaviour."""
+    ref = "/root/reference/rep_queue.h"
+    if not os.path.exists(ref):
+        pytest.skip("the reference's rep_queue.h is not here")
+    exe = tmp_path / "glue_drain_asan"
+    subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration"),
+                    "-I", os.path.dirname(ref), "-o", str(exe), os.path.join(ROOT, "tests", "glue", "drain_main.c"),
+                    os.path.join(ROOT, "integration", "cocytus_drain.c"), "-L", os.path.join(ROOT, "cocytus_amd"),
+                    "-lcocytus_ec", "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd")], check=True)
+    global EXE
+    saved, EXE = EXE, str(exe)
+    os.environ["ASAN_OPTIONS"] = "detect_leaks=0"
+    try:
+        test_collect_window_ring_and_lengths(tmp_path)
+        test_collect_refuses_gaps_and_overflow(tmp_path)
+    finally:
+        EXE = saved
+        os.environ.pop("ASAN_OPTIONS", None)
