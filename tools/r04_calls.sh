@@ -59,4 +59,13 @@ f)
   run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   EVID_NO_PROF=1 timeout -k 10 900 bash tools/round_evidence.sh r04f
   ;;
+g)
+  # rocprofv3 --kernel-trace --stats of the driver's exact command (python bench.py, no
+  # flags) with its line, so the line's encode launch time can be checked against the
+  # trace's whole-batch encode dispatches of the same run (tools/trace_check.py)
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_default" -o run \
+      --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" > "$GRAFT_REPO_ROOT/gpurun_out/r04g/bench_default.jsonl" \
+      2> "$GRAFT_REPO_ROOT/gpurun_out/r04g/bench_default.err"
+  ;;
 esac
