@@ -7,7 +7,7 @@
 `rocprofv3 --kernel-trace --stats`.  The line's `roofline.launch_ms` is the average
 HIP-event time of its timed whole-batch encode launches; here the same launches are
 picked out of the trace -- the first (warmup + steps) dispatches of the line's encode
-kernel with the whole batch's grid, in start order (the metric's workload runs first;
+kernel with the whole batch's grid (256 work-items per 4 KiB tile), in start order (the metric's workload runs first;
 later whole-batch dispatches of that kernel belong to other workloads), the last `steps`
 of them timed -- and their average duration is compared with the line's.
 """
@@ -40,7 +40,7 @@ def main(prof_dir, line_path, out_path=None):
         return int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
 
     enc = sorted((r for r in rows if is_encode(r)), key=lambda r: int(r["Start_Timestamp"]))
-    whole = max(grid(r) for r in enc)  # the whole batch: the largest grid of this kernel
+    whole = tiles * 256  # one 4 KiB tile = 256 lanes (in 1, 2 or 4 workgroups): the whole batch
     batch = [r for r in enc if grid(r) == whole][: warm + steps]
     timed = batch[warm:]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
