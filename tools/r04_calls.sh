@@ -68,4 +68,10 @@ g)
       --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" > "$GRAFT_REPO_ROOT/gpurun_out/r04g/bench_default.jsonl" \
       2> "$GRAFT_REPO_ROOT/gpurun_out/r04g/bench_default.err"
   ;;
+h)
+  # the final tree as the driver runs it: smoke, the GPU suite, the default line
+  run smoke 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+  run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  run bench_default 300 python -u bench.py
+  ;;
 esac
