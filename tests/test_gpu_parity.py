@@ -258,6 +258,41 @@ def test_diff_update(gpu, oracle, engine, k, m, install):
             assert np.array_equal(enc[p], parity[p])
 
 
+@pytest.mark.parametrize("engine_name", ["auto", "perm", "lds"])
+def test_diff_update_full_size(gpu, oracle, engine_name):
+    """The north star's per-SET diff-update at the bench's size (65,536 SETs of
+    4 KiB, source shard j uniform in {0,1,2}, RS(3,2), install), three rounds of new
+    values: the parity arenas stay the encode of the installed data (a size-independent
+    property), checked against the oracle's encode of the whole 256 MiB arenas; and the
+    installed data equal the last round's values."""
+    torch, ec = gpu
+    k, m, n, B = 3, 2, 4096, 65536
+    T = n * B
+    mat = ec.coding_matrix(k, m)
+    g = torch.Generator(device="cuda").manual_seed(0xC0C70006)
+    data = [torch.randint(0, 256, (T,), dtype=torch.uint8, device="cuda", generator=g) for _ in range(k)]
+    parity = [torch.empty(T, dtype=torch.uint8, device="cuda") for _ in range(m)]
+    ec.encode_region(k, m, mat, data, parity, T)
+    src = np.random.default_rng(6).integers(0, k, B)
+    default = ec.get_engine()
+    ec.set_engine({"auto": ec.CEC_ENGINE_AUTO, "perm": ec.CEC_ENGINE_PERM, "lds": ec.CEC_ENGINE_LDS}[engine_name])
+    try:
+        with ec.Plan([(s * n, s * n, n, int(src[s])) for s in range(B)]) as plan:
+            for _ in range(3):
+                stage = torch.randint(0, 256, (T,), dtype=torch.uint8, device="cuda", generator=g)
+                ec.diff_update(k, m, mat, data, stage, parity, True, plan)
+                ran = ec.last_engine()
+            torch.cuda.synchronize()
+    finally:
+        ec.set_engine(default)
+    if engine_name == "auto":
+        assert ran == ec.CEC_ENGINE_PERM
+    for j in range(k):  # each SET installed the last round's value into its own shard only
+        sel = torch.from_numpy(np.repeat(src == j, n)).cuda()
+        assert torch.equal(torch.where(sel, stage, data[j]), data[j]), f"install {j}"
+    _assert_parity_matches_oracle(torch, oracle, mat, k, m, data, parity)
+
+
 def test_diff_update_lost_parity_and_overlap(gpu, oracle):
     torch, ec = gpu
     k, m = 3, 2

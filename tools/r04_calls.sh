@@ -74,4 +74,8 @@ h)
   run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
   run bench_default 300 python -u bench.py
   ;;
+i)
+  # the diff-update at the bench's size under each engine
+  run du_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_diff_update_full_size
+  ;;
 esac
