@@ -564,6 +564,32 @@ def test_drainer_matches_sequential_loop(gpu, oracle, engine, staging):
     assert np.array_equal(to_host(dev), parity)
 
 
+def test_drainer_full_size(gpu, oracle):
+    """The batched drain at the bench's size: 65,536 pending 4 KiB
+    diffs in pageable host memory, source shard uniform in {0,1,2}, addresses shuffled
+    over a 256 MiB parity arena, applied by one cec_drainer_apply (64 MiB staging: several
+    rounds) == the reference's sequential drain loop (memcached.c:4350 -> 7764) run by the
+    oracle over the same diffs."""
+    torch, ec = gpu
+    k, m, n, N = 3, 2, 4096, 65536
+    mat = ec.coding_matrix(k, m)
+    lid_self = k + 1
+    rng = np.random.default_rng(0xC0C70001)
+    diffs = rng.integers(0, 256, N * n, dtype=np.uint8)
+    src = rng.integers(0, k, N)
+    addrs = rng.permutation(N).astype(np.uint64) * n
+    parity0 = rng.integers(0, 256, N * n, dtype=np.uint8)
+    parity = to_dev(torch, parity0)
+    with ec.Drainer(k, m, mat, lid_self, staging_bytes=64 << 20) as d:
+        launches = d.apply([(diffs[i * n:(i + 1) * n], int(addrs[i]), int(src[i])) for i in range(N)], parity)
+    torch.cuda.synchronize()
+    want = parity0.copy()
+    oracle.bench_apply(diffs, np.arange(N, dtype=np.uint64) * n, addrs, np.full(N, n),
+                       [mat[lid_self * k + int(j)] for j in src], want)
+    assert launches >= 4  # 256 MiB of diffs through 64 MiB of staging
+    assert torch.equal(parity, to_dev(torch, want))
+
+
 def test_drainer_in_place_staging(gpu, oracle):
     """Diffs received straight into the drainer's pinned staging are applied without the
     pack copy (overlapping and ragged ones included), same bytes as the sequential loop."""

@@ -76,6 +76,6 @@ h)
   ;;
 i)
   # the diff-update at the bench's size under each engine
-  run du_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_diff_update_full_size
+  run du_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_diff_update_full_size tests/test_gpu_parity.py::test_drainer_full_size
   ;;
 esac
