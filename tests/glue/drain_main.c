@@ -7,6 +7,10 @@
  *                               collected update "entry addr len lid", or "rc N"
  *   drain_main apply IN OUT     GPU: cocytus_drain_gf into a device parity arena that
  *                               starts from IN's parity bytes; OUT = the arena afterwards
+ *   drain_main bench N SIZE     GPU: N queued SIZE-byte diffs of one peer drained (a) by
+ *                               cocytus_drain_gf into a device arena, (b) by the unchanged
+ *                               loop through the drop-in (one galois_w08_region_multiply
+ *                               per xid into a host ecmem, memcached.c:7764); one JSON line
  *
  * IN (little-endian): int32 lid, self_lid, k, m, ring_cap, tail, n_entries, arena_bytes,
  * cap; uint64 done_xid, stable_xid; n_entries x {uint64 xid, uint64 addr, int32 len,
@@ -17,8 +21,10 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include <cocytus_ec.h>
+#include <galois.h>
 #include <reed_sol.h>
 
 #include "cocytus_drain.h"
@@ -52,7 +58,105 @@ static void rd(FILE *f, void *p, size_t n) {
     }
 }
 
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static uint32_t plain_nbytes(void *item, void *ctx) {
+    (void)ctx;
+    return *(uint32_t *)item;
+}
+
+/* Server-level drain rate: the glue against the unchanged per-xid loop on the shim. */
+static int bench(int n, int size) {
+    const int K = 3, M = 2, lid = 1, self = K + 1;
+    const size_t arena = (size_t)n * (size_t)size;
+    struct rep_queue q;
+    q.cap = (uint32_t)n;
+    q.items = calloc((size_t)n, sizeof(struct rep_queue_item));
+    q.tail = 0;
+    q.head = (uint32_t)n;
+    uint32_t nbytes = (uint32_t)size;
+    uint64_t seed = 0x9E3779B97F4A7C15ull;
+    for (int e = 0; e < n; ++e) { /* addresses shuffled over the arena, as ecalloc reuses */
+        struct rep_queue_item *it = &q.items[e];
+        it->xid = (uint64_t)e + 1;
+        it->lid = lid;
+        it->vbuf = malloc((size_t)size);
+        it->vnbytes = size;
+        it->item = &nbytes;
+        for (int b = 0; b < size; b += 8) {
+            seed ^= seed << 13, seed ^= seed >> 7, seed ^= seed << 17;
+            memcpy(it->vbuf + b, &seed, size - b >= 8 ? 8 : (size_t)(size - b));
+        }
+    }
+    for (int e = n - 1; e > 0; --e) { /* Fisher-Yates over the slots */
+        seed ^= seed << 13, seed ^= seed >> 7, seed ^= seed << 17;
+        const int r = (int)(seed % (uint64_t)(e + 1));
+        q.items[e].addr = (uint64_t)r; /* temp: permutation built below */
+    }
+    int *perm = malloc(sizeof(int) * (size_t)n);
+    for (int e = 0; e < n; ++e) perm[e] = e;
+    for (int e = n - 1; e > 0; --e) {
+        const int r = (int)q.items[e].addr, t = perm[e];
+        perm[e] = perm[r];
+        perm[r] = t;
+    }
+    for (int e = 0; e < n; ++e) q.items[e].addr = (uint64_t)perm[e] * (uint64_t)size;
+    if (cec_device_check() != CEC_OK) return 2;
+    int *matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
+    uint8_t *parity;
+    void *slab;
+    cec_drainer *dr;
+    uint8_t *ecmem = calloc(arena, 1); /* the host ecmem of the unchanged loop; zeros */
+    if (cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, ecmem, arena, NULL) ||
+        cec_stream_synchronize(NULL) || cec_drainer_create(&dr, K, M, matrix, self, 64u << 20))
+        return 2;
+    cec_host_update *scratch = calloc((size_t)n, sizeof *scratch);
+    cocytus_drain_hooks hooks = {plain_nbytes, NULL, NULL};
+    double best = 1e30, t_sum = 0;
+    const int reps = 4; /* + one warm-up: 5 drains, an odd count, so the arena holds each diff once */
+    for (int r = 0; r < reps + 1; ++r) {
+        const double t0 = now_s();
+        const int rc = cocytus_drain_gf(&q, lid, 0, (uint64_t)n, &hooks, dr, parity, NULL, scratch, n);
+        const double t = now_s() - t0;
+        if (rc != n) return 3;
+        if (r) {
+            t_sum += t;
+            if (t < best) best = t;
+        }
+    }
+    /* the unchanged server: one drop-in call per xid into a host ecmem (memcached.c:7764);
+     * a first call (and its undo: XOR twice) sets the drop-in's stream and staging up */
+    const int c = matrix[self * K + lid];
+    galois_w08_region_multiply(q.items[0].vbuf, c, size, (char *)ecmem, 1);
+    galois_w08_region_multiply(q.items[0].vbuf, c, size, (char *)ecmem, 1);
+    const double t1 = now_s();
+    for (int e = 0; e < n; ++e)
+        galois_w08_region_multiply(q.items[e].vbuf, c, size, (char *)ecmem + q.items[e].addr, 1);
+    const double t_loop = now_s() - t1;
+    /* both paths applied every diff once: the same bytes, and not all zero */
+    uint8_t *dev_copy = malloc(arena);
+    if (cec_copy(dev_copy, parity, arena, NULL) || cec_stream_synchronize(NULL)) return 2;
+    int nonzero = 0;
+    for (size_t i = 0; i < arena && !nonzero; ++i) nonzero = ecmem[i] != 0;
+    const int ok = nonzero && memcmp(dev_copy, ecmem, arena) == 0;
+    const double gib = (double)arena / (double)(1u << 30);
+    printf("{\"path\": \"server drain loop over the real rep_queue: %d queued %d-byte diffs of one peer\", "
+           "\"glue_GiBps\": %.2f, \"glue_runs\": %d, \"glue_ms_mean\": %.3f, \"glue_ms_best\": %.3f, "
+           "\"dropin_loop_GiBps\": %.3f, \"dropin_loop_ms\": %.1f, \"dropin_us_per_xid\": %.2f, "
+           "\"speedup\": %.1f, \"launches\": %d, \"verified\": %s}\n",
+           n, size, gib / (t_sum / reps), reps, 1e3 * t_sum / reps, 1e3 * best, gib / t_loop, 1e3 * t_loop,
+           1e6 * t_loop / n, t_loop / (t_sum / reps), cec_drainer_last_launches(dr), ok ? "true" : "false");
+    cec_drainer_destroy(dr);
+    cec_arenas_free(slab);
+    return ok ? 0 : 4;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 4 && !strcmp(argv[1], "bench")) return bench(atoi(argv[2]), atoi(argv[3]));
     if (argc != 4) return 1;
     const int apply = !strcmp(argv[1], "apply");
     FILE *in = fopen(argv[2], "rb");

@@ -78,4 +78,10 @@ i)
   # the diff-update at the bench's size under each engine
   run du_tests 600 $PYT -m gpu tests/test_gpu_parity.py::test_diff_update_full_size tests/test_gpu_parity.py::test_drainer_full_size
   ;;
+j)
+  # the drain loop at the server level over the real rep_queue: the glue vs the unchanged
+  # per-xid loop through the drop-in (4098 B = a 4 KiB value + CRLF, memcached.c:3610)
+  run glue_bench 300 oracle/_ref/glue_drain bench 65536 4098
+  run glue_bench_4k 300 oracle/_ref/glue_drain bench 65536 4096
+  ;;
 esac

@@ -27,6 +27,10 @@ timeout -k 10 200 tools/hbm_mix.bin arena random 64  > "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/hbm_mix.bin arena random 256 >> "$OUT/hbm_mix.txt" 2>&1
 timeout -k 10 200 tools/dropin_latency.bin > "$OUT/dropin_latency.jsonl" 2>&1
 timeout -k 10 200 tools/pool_bench.bin     > "$OUT/pool_bench.jsonl" 2>&1
+# the drain loop at the server level, over the real rep_queue (oracle/_ref, built here)
+if [ -x oracle/_ref/glue_drain ]; then
+  timeout -k 10 200 oracle/_ref/glue_drain bench 65536 4098 > "$OUT/glue_drain_bench.jsonl" 2>&1
+fi
 timeout -k 10 200 tools/launch_latency.bin > "$OUT/launch_latency.txt" 2>&1
 timeout -k 10 200 tools/bench_native.bin 20 3 > "$OUT/bench_native.jsonl" 2>&1
 for b in 32768 16384 8192; do  # the strong-scaling shares with no Python in the loop
