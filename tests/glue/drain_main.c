@@ -7,10 +7,11 @@
  *                               collected update "entry addr len lid", or "rc N"
  *   drain_main apply IN OUT     GPU: cocytus_drain_gf into a device parity arena that
  *                               starts from IN's parity bytes; OUT = the arena afterwards
- *   drain_main bench N SIZE     GPU: N queued SIZE-byte diffs of one peer drained (a) by
+ *   drain_main bench N SIZE [MB] GPU: N queued SIZE-byte diffs of one peer drained (a) by
  *                               cocytus_drain_gf into a device arena, (b) by the unchanged
  *                               loop through the drop-in (one galois_w08_region_multiply
- *                               per xid into a host ecmem, memcached.c:7764); one JSON line
+ *                               per xid into a host ecmem, memcached.c:7764); one JSON line;
+ *                               MB: the drainer's staging (default 64 MiB)
  *
  * IN (little-endian): int32 lid, self_lid, k, m, ring_cap, tail, n_entries, arena_bytes,
  * cap; uint64 done_xid, stable_xid; n_entries x {uint64 xid, uint64 addr, int32 len,
@@ -70,7 +71,7 @@ static uint32_t plain_nbytes(void *item, void *ctx) {
 }
 
 /* Server-level drain rate: the glue against the unchanged per-xid loop on the shim. */
-static int bench(int n, int size) {
+static int bench(int n, int size, int staging_mb) {
     const int K = 3, M = 2, lid = 1, self = K + 1;
     const size_t arena = (size_t)n * (size_t)size;
     struct rep_queue q;
@@ -112,7 +113,7 @@ static int bench(int n, int size) {
     cec_drainer *dr;
     uint8_t *ecmem = calloc(arena, 1); /* the host ecmem of the unchanged loop; zeros */
     if (cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, ecmem, arena, NULL) ||
-        cec_stream_synchronize(NULL) || cec_drainer_create(&dr, K, M, matrix, self, 64u << 20))
+        cec_stream_synchronize(NULL) || cec_drainer_create(&dr, K, M, matrix, self, (size_t)staging_mb << 20))
         return 2;
     cec_host_update *scratch = calloc((size_t)n, sizeof *scratch);
     cocytus_drain_hooks hooks = {plain_nbytes, NULL, NULL};
@@ -145,10 +146,11 @@ static int bench(int n, int size) {
     const int ok = nonzero && memcmp(dev_copy, ecmem, arena) == 0;
     const double gib = (double)arena / (double)(1u << 30);
     printf("{\"path\": \"server drain loop over the real rep_queue: %d queued %d-byte diffs of one peer\", "
+           "\"staging_MiB\": %d, "
            "\"glue_GiBps\": %.2f, \"glue_runs\": %d, \"glue_ms_mean\": %.3f, \"glue_ms_best\": %.3f, "
            "\"dropin_loop_GiBps\": %.3f, \"dropin_loop_ms\": %.1f, \"dropin_us_per_xid\": %.2f, "
            "\"speedup\": %.1f, \"launches\": %d, \"verified\": %s}\n",
-           n, size, gib / (t_sum / reps), reps, 1e3 * t_sum / reps, 1e3 * best, gib / t_loop, 1e3 * t_loop,
+           n, size, staging_mb, gib / (t_sum / reps), reps, 1e3 * t_sum / reps, 1e3 * best, gib / t_loop, 1e3 * t_loop,
            1e6 * t_loop / n, t_loop / (t_sum / reps), cec_drainer_last_launches(dr), ok ? "true" : "false");
     cec_drainer_destroy(dr);
     cec_arenas_free(slab);
@@ -156,7 +158,8 @@ static int bench(int n, int size) {
 }
 
 int main(int argc, char **argv) {
-    if (argc == 4 && !strcmp(argv[1], "bench")) return bench(atoi(argv[2]), atoi(argv[3]));
+    if ((argc == 4 || argc == 5) && !strcmp(argv[1], "bench"))
+        return bench(atoi(argv[2]), atoi(argv[3]), argc == 5 ? atoi(argv[4]) : 64);
     if (argc != 4) return 1;
     const int apply = !strcmp(argv[1], "apply");
     FILE *in = fopen(argv[2], "rb");

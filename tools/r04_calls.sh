@@ -83,5 +83,6 @@ j)
   # per-xid loop through the drop-in (4098 B = a 4 KiB value + CRLF, memcached.c:3610)
   run glue_bench 300 oracle/_ref/glue_drain bench 65536 4098
   run glue_bench_4k 300 oracle/_ref/glue_drain bench 65536 4096
+  run glue_bench_256 300 oracle/_ref/glue_drain bench 65536 4098 256
   ;;
 esac
