@@ -34,6 +34,20 @@ SHAPES = {"rs32_4k": ("<3, 2,", "<3, 1,"), "rs42_64k": ("<4, 2,", "<4, 1,"), "rs
 OPS = {"rs32_diff_update": ("diff_update", None)}  # op names of (first, second) shape
 
 
+def sources_sha256() -> str:
+    """sha256 (16 hex digits) of the library's sources (cocytus_amd/csrc/*, include/*) when
+    the summary is written, for the record; bench.py keys on kernel_code_id (the device
+    code the counters measured), which host-only edits leave unchanged."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for d in ("cocytus_amd/csrc", "include"):
+        for name in sorted(os.listdir(os.path.join(ROOT, d))):
+            with open(os.path.join(ROOT, d, name), "rb") as f:
+                h.update(name.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def one(path_glob):
     c = glob.glob(path_glob, recursive=True)
     return c[0] if c else None
@@ -118,7 +132,8 @@ def main(out, rnd, engine="perm"):
     # while the library it loads has the same device code (traffic_stale otherwise).
     from cocytus_amd import ec
 
-    traffic["_build"] = {"kernel_code_id": ec.kernel_code_id(), "round": rnd, "engine": engine}
+    traffic["_build"] = {"kernel_code_id": ec.kernel_code_id(), "sources_sha256": sources_sha256(),
+                         "round": rnd, "engine": engine}
     with open(os.path.join(prof, "pmc_traffic.json" if engine == "perm" else f"pmc_traffic_{engine}.json"),
               "w") as f:
         json.dump(traffic, f, indent=1)
