@@ -226,31 +226,53 @@ def cpu_thread_counts(allowed: int) -> list[int]:
 CPU_SAMPLES = 5  # timed passes per thread count, after one warm-up pass
 
 
-def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES):
+def cpu_allowed(h=None) -> int:
+    """CPUs this process may run threads on: its affinity, capped at the cgroup quota
+    (threads beyond the quota only time-slice)."""
+    h = h or host_cpu()
+    allowed = h["affinity"] or os.cpu_count() or 1
+    if h["cpu_quota"]:
+        allowed = max(1, min(allowed, math.ceil(h["cpu_quota"])))
+    return allowed
+
+
+CPU_OTHER_S = 3.0  # CPU-baseline budget per other workload (top thread count only)
+
+
+def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES, sizes=None):
     """Oracle (restated Jerasure/GF-Complete, AVX2) on the host cores, bounded samples.
 
     One pthread per CPU on disjoint stripes, swept over cpu_thread_counts(); at each
     point the batch is filled once, one pass warms up, then `samples` timed passes of
     about wall_s / len(sweep) / (samples + 1) seconds each: median, min and max.
     `value` / `cores` is the median of the all-CPU point (the host's ceiling);
-    `reference_config` is the 1-thread point (the reference's configuration)."""
+    `reference_config` is the 1-thread point (the reference's configuration).
+    sizes: the value lengths of a mixed batch (the whole batch, instead of 256 MiB of
+    n-byte stripes per shard); n is then ignored."""
     from oracle import pyoracle
 
     h = host_cpu()
-    allowed = h["affinity"] or os.cpu_count() or 1
-    if h["cpu_quota"]:  # threads beyond the cgroup's CPU quota only time-slice
-        allowed = max(1, min(allowed, math.ceil(h["cpu_quota"])))
-    counts = threads_list or cpu_thread_counts(allowed)
+    counts = threads_list or cpu_thread_counts(cpu_allowed(h))
     per_point = max(0.2, wall_s / len(counts))
-    stripes = (256 << 20) // n  # 256 MiB per shard, 1.25 GiB for RS(3,2): above any LLC
-    payload = (k + 1) * n * stripes  # K*n encoded + n rebuilt per stripe, as the GPU metric
+    if sizes is None:
+        stripes = (256 << 20) // n  # 256 MiB per shard, 1.25 GiB for RS(3,2): above any LLC
+        payload = (k + 1) * n * stripes  # K*n encoded + n rebuilt per stripe, as the GPU metric
+
+        def run(T, reps, count):
+            return pyoracle.bench_encode_decode_samples(k, m, n, stripes, T, reps, count, True)
+    else:
+        stripes = len(sizes)
+        payload = (k + 1) * sum(sizes)
+
+        def run(T, reps, count):
+            return pyoracle.bench_encode_decode_sizes(k, m, sizes, T, reps, count, True)
     simd = "AVX2" if pyoracle.simd_available() else "scalar"
     sweep = []
     for T in counts:
         # calibrate: one pass after a warm-up pass (fill untimed)
-        t1 = pyoracle.bench_encode_decode_samples(k, m, n, stripes, T, 1, 2, True)[1]
+        t1 = run(T, 1, 2)[1]
         reps = max(1, min(1000, int(per_point / (samples + 1) / max(t1, 1e-6))))
-        ts = pyoracle.bench_encode_decode_samples(k, m, n, stripes, T, reps, samples + 1, True)[1:]
+        ts = run(T, reps, samples + 1)[1:]
         vals = sorted(round(payload * reps / t / 2**30, 3) for t in ts)
         sweep.append({"threads": T, "value": statistics.median(vals), "median": statistics.median(vals),
                       "min": vals[0], "max": vals[-1], "samples": vals, "passes_per_sample": reps,
@@ -267,7 +289,9 @@ def cpu_baseline(k, m, n, wall_s, threads_list=None, samples=CPU_SAMPLES):
         "kind": "port",
         "label": "restated CPU baseline",  # Jerasure / GF-Complete absent
         "median": top["median"], "min": top["min"], "max": top["max"], "samples": top["samples"],
-        "sample": f"RS({k},{m}) encode+decode of {stripes} x {n} B stripes on {top['threads']} threads: "
+        "sample": f"RS({k},{m}) encode+decode of {stripes} x "
+                  f"{'%d B' % n if sizes is None else 'mixed 256 B - 1 MiB (the GPU batch)'} stripes on "
+                  f"{top['threads']} threads: "
                   f"median of {samples} timed passes ({top['passes_per_sample']} repetitions each) after "
                   f"one warm-up pass; every CPU this process may use (affinity {h['affinity']}, cgroup "
                   f"quota {h['cpu_quota']}), the host's ceiling for it; restated GF-Complete SPLIT(8,4) "
@@ -894,6 +918,15 @@ def run_device(args):
         }
         if w == "rs32_4k_lds":
             also[w]["kernel"] = o["roofline"]["kernel"]
+        elif world == 1 and not args.no_cpu_baseline:
+            # BASELINE.md §2's other CPU-baseline configs, beside the GPU number: the same
+            # restated path on every CPU this process may use, over the same value sizes
+            # (the mixed batch itself; 256 MiB per shard of n-byte values otherwise)
+            cb = cpu_baseline(o["k"], o["m"], o["n"] or 4096, CPU_OTHER_S, threads_list=[cpu_allowed()],
+                              sizes=None if o["n"] else [ln for _, ln in layout(w)[0]])
+            also[w]["cpu_baseline"] = {x: cb[x] for x in ("value", "unit", "cores", "kind", "label", "median",
+                                                          "min", "max", "sample")}
+            also[w]["gpu_over_cpu"] = round(o["value"] / cb["value"], 1)
     # per-rank evidence, outside every timed region: device identity and own times
     mine = {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
             "identity": device_identity(torch, torch.cuda.current_device()),

@@ -81,6 +81,7 @@ typedef struct {
     const int *matrix;
     int k, m, do_decode, reps, samples;
     long n, s0, s1;
+    const long *offs, *lens; /* per-stripe offset / length (mixed sizes), or NULL: s * n, n */
     uint8_t **data, **parity, *out, *res;
     pthread_barrier_t *bar;
 } bench_arg;
@@ -107,17 +108,20 @@ static void *bench_worker(void *p)
 {
     bench_arg *a = (bench_arg *)p;
     const int k = a->k, m = a->m;
-    const long n = a->n;
     /* each thread fills and first-touches its own stripes (NUMA-local pages on a
      * multi-socket host); untimed */
-    const size_t lo = (size_t)a->s0 * (size_t)n, hi = (size_t)a->s1 * (size_t)n;
+    const int none = a->s1 <= a->s0; /* more threads than stripes: nothing to fill */
+    const size_t lo = none ? 0 : a->offs ? (size_t)a->offs[a->s0] : (size_t)a->s0 * (size_t)a->n;
+    const size_t hi = none ? 0
+                      : a->offs ? (size_t)(a->offs[a->s1 - 1] + a->lens[a->s1 - 1])
+                                : (size_t)a->s1 * (size_t)a->n;
     for (int j = 0; j < k; ++j) fill_splitmix(a->data[j], 0xC0C70001ull + (uint64_t)j, lo, hi);
     for (int q = 0; q < m; ++q) memset(a->parity[q] + lo, 0, hi - lo);
     pthread_barrier_wait(a->bar);
     for (int smp = 0; smp < a->samples; ++smp) {
     for (int r = 0; r < a->reps; ++r) {
         for (long s = a->s0; s < a->s1; ++s) {
-            const long off = s * n;
+            const long off = a->offs ? a->offs[s] : s * a->n, n = a->lens ? a->lens[s] : a->n;
             for (int q = 0; q < m; ++q) memset(a->parity[q] + off, 0, (size_t)n);
             for (int j = 0; j < k; ++j)
                 for (int q = 0; q < m; ++q)
@@ -143,14 +147,30 @@ static void *bench_worker(void *p)
 /* `samples` timed passes of `reps` repetitions each over the same filled stripes
  * (one fill, untimed); t[i] = seconds of sample i (CLOCK_MONOTONIC between the
  * barriers that end consecutive samples: every thread has finished it). */
-int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int threads,
-                                    int reps, int do_decode, int samples, double *t)
+/* lens != NULL: stripe s has lens[s] bytes (mixed sizes, SURVEY §8d cfg 3), packed at
+ * 16-B aligned offsets (ecalloc.c:176); threads split the stripes by bytes; n is then
+ * ignored.  lens == NULL: every stripe has n bytes. */
+int ref_bench_encode_decode_sizes(int k, int m, long n, const long *lens, long nstripes, int threads,
+                                  int reps, int do_decode, int samples, double *t)
 {
     if (threads < 1) threads = 1;
-    if (samples < 1 || !t) return -1;
+    if (samples < 1 || !t || nstripes < 1) return -1;
     int *matrix = ref_big_vandermonde(k + m, k);
     uint8_t *data[32], *parity[32];
-    const size_t bytes = (size_t)n * (size_t)nstripes;
+    long *offs = NULL;
+    size_t bytes = (size_t)n * (size_t)nstripes;
+    long maxlen = n;
+    if (lens) {
+        offs = (long *)malloc(sizeof(long) * (size_t)nstripes);
+        long o = 0;
+        maxlen = 0;
+        for (long s = 0; s < nstripes; ++s) {
+            offs[s] = o;
+            o = (o + lens[s] + 15) & ~15L;
+            if (lens[s] > maxlen) maxlen = lens[s];
+        }
+        bytes = (size_t)o;
+    }
     /* filled by the workers, each its own stripes (bench_worker) */
     for (int j = 0; j < k; ++j) data[j] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
     for (int q = 0; q < m; ++q) parity[q] = (uint8_t *)aligned_alloc(64, (bytes + 63) & ~(size_t)63);
@@ -162,11 +182,21 @@ int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int thr
         bench_arg *a = &args[th];
         a->matrix = matrix; a->k = k; a->m = m; a->n = n; a->reps = reps; a->do_decode = do_decode;
         a->samples = samples;
-        a->s0 = nstripes * th / threads;
-        a->s1 = nstripes * (th + 1) / threads;
+        a->offs = offs; a->lens = lens;
+        if (lens) { /* by bytes: the first stripe starting at or past th / threads of them */
+            long lo = 0, hi = 0;
+            while (lo < nstripes && (size_t)offs[lo] * (size_t)threads < bytes * (size_t)th) ++lo;
+            hi = lo;
+            while (hi < nstripes && (size_t)offs[hi] * (size_t)threads < bytes * (size_t)(th + 1)) ++hi;
+            a->s0 = lo;
+            a->s1 = th + 1 == threads ? nstripes : hi;
+        } else {
+            a->s0 = nstripes * th / threads;
+            a->s1 = nstripes * (th + 1) / threads;
+        }
         a->data = data; a->parity = parity; a->bar = &bar;
-        a->out = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
-        a->res = (uint8_t *)aligned_alloc(64, ((size_t)n + 63) & ~(size_t)63);
+        a->out = (uint8_t *)aligned_alloc(64, ((size_t)maxlen + 63) & ~(size_t)63);
+        a->res = (uint8_t *)aligned_alloc(64, ((size_t)maxlen + 63) & ~(size_t)63);
         pthread_create(&tid[th], NULL, bench_worker, a);
     }
     struct timespec t0, t1;
@@ -182,9 +212,15 @@ int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int thr
     for (int th = 0; th < threads; ++th) { free(args[th].out); free(args[th].res); }
     for (int j = 0; j < k; ++j) free(data[j]);
     for (int q = 0; q < m; ++q) free(parity[q]);
-    free(args); free(tid); free(matrix);
+    free(args); free(tid); free(matrix); free(offs);
     pthread_barrier_destroy(&bar);
     return 0;
+}
+
+int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int threads,
+                                    int reps, int do_decode, int samples, double *t)
+{
+    return ref_bench_encode_decode_sizes(k, m, n, NULL, nstripes, threads, reps, do_decode, samples, t);
 }
 
 double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,

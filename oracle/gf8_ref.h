@@ -124,6 +124,11 @@ double ref_bench_encode_decode(int k, int m, long n, long nstripes, int threads,
  * t[i] = seconds of pass i (the first is the caller's warm-up). 0, or -1 on bad args. */
 int ref_bench_encode_decode_samples(int k, int m, long n, long nstripes, int threads,
                                     int reps, int do_decode, int samples, double *t);
+/* The same with per-stripe lengths lens[s] (mixed value sizes, SURVEY §8d cfg 3), packed
+ * at 16-B aligned offsets as ecalloc.c:176 places them; threads split by bytes.  lens ==
+ * NULL is the uniform-n form above. */
+int ref_bench_encode_decode_sizes(int k, int m, long n, const long *lens, long nstripes, int threads,
+                                  int reps, int do_decode, int samples, double *t);
 
 /* The parity's drain loop as the reference runs it (one thread, memcached.c:4350 ->
  * process_rep_command -> galois_w08_region_multiply(diff, MATRIX(self, lid), n,

@@ -44,6 +44,8 @@ _SIGS = {
     "ref_simd_available": ([], _i),
     "ref_bench_encode_decode": ([_i, _i, _l, _l, _i, _i, _i], ctypes.c_double),
     "ref_bench_encode_decode_samples": ([_i, _i, _l, _l, _i, _i, _i, _i, ctypes.POINTER(ctypes.c_double)], _i),
+    "ref_bench_encode_decode_sizes": ([_i, _i, _l, ctypes.c_void_p, _l, _i, _i, _i, _i,
+                                       ctypes.POINTER(ctypes.c_double)], _i),
     "ref_bench_apply": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                          ctypes.c_void_p, _i, ctypes.c_void_p], ctypes.c_double),
     "ref_bench_recover": ([ctypes.c_void_p, _vpp, ctypes.c_void_p, _i, _i, _l, ctypes.c_void_p,
@@ -203,6 +205,16 @@ def bench_encode_decode_samples(k, m, n, nstripes, threads, reps, samples, do_de
     t = (ctypes.c_double * samples)()
     if lib().ref_bench_encode_decode_samples(k, m, n, nstripes, threads, reps, int(do_decode), samples, t):
         raise ValueError("ref_bench_encode_decode_samples: bad arguments")
+    return list(t)
+
+
+def bench_encode_decode_sizes(k, m, lens, threads, reps, samples, do_decode=True) -> list[float]:
+    """bench_encode_decode_samples over stripes of the given lengths (mixed value sizes)."""
+    ln = np.ascontiguousarray(lens, np.int64)
+    t = (ctypes.c_double * samples)()
+    if lib().ref_bench_encode_decode_sizes(k, m, 0, ln.ctypes.data, len(ln), threads, reps, int(do_decode),
+                                           samples, t):
+        raise ValueError("ref_bench_encode_decode_sizes: bad arguments")
     return list(t)
 
 

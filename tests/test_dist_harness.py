@@ -208,6 +208,38 @@ def test_cpu_baseline_small():
     assert cb["value"] == cb["median"] == cb["sweep"][-1]["median"]
 
 
+def test_cpu_baseline_mixed_sizes():
+    """The CPU-baseline leg over a mixed batch's own value sizes (BASELINE.md §2 config
+    (2)): the same restated path, payload = (K+1) x the batch's bytes, threads split by
+    bytes; a uniform batch through the sizes form matches the uniform form's work."""
+    import bench
+    from oracle import pyoracle
+
+    sizes = [ln for _, ln in bench.layout("rs32_mixed")[0]][:400]
+    cb = bench.cpu_baseline(3, 2, 4096, 0.3, threads_list=[2], sizes=sizes)
+    assert cb["value"] > 0 and cb["cores"] == 2 and "mixed" in cb["sample"]
+    assert len(cb["samples"]) == bench.CPU_SAMPLES
+    # every thread count, including more threads than stripes, runs and times the batch
+    for T in (1, 3, 500):
+        assert all(t > 0 for t in pyoracle.bench_encode_decode_sizes(3, 2, sizes[:7], T, 1, 2))
+
+
+def test_cpu_baseline_split_under_asan(tmp_path):
+    """The oracle's CPU-baseline workers (oracle/gf8_cpu_baseline.c) split stripes over
+    threads by count or by bytes; under AddressSanitizer + UBSan, with more threads than
+    stripes and mixed sizes, no access leaves the batch."""
+    import subprocess
+
+    exe = tmp_path / "bench_sizes"
+    subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-std=gnu11", "-mavx2", "-o", str(exe),
+                    os.path.join(ROOT, "tests", "oracle_c", "bench_sizes_main.c"),
+                    os.path.join(ROOT, "oracle", "gf8_ref.c"), os.path.join(ROOT, "oracle", "gf8_cpu_baseline.c"),
+                    "-lpthread"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
+
+
 def test_shard_stripes_by_count_and_by_bytes():
     """contiguous split by stripe count for one value size, by byte count for
     mixed sizes; the shares tile the batch exactly."""
