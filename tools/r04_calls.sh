@@ -85,4 +85,8 @@ j)
   run glue_bench_4k 300 oracle/_ref/glue_drain bench 65536 4096
   run glue_bench_256 300 oracle/_ref/glue_drain bench 65536 4098 256
   ;;
+k)
+  # the default line with the other configs' CPU baselines
+  run bench_default 400 python -u bench.py
+  ;;
 esac
