@@ -177,13 +177,22 @@ int main(int argc, char **argv) {
     q.tail = (uint32_t)tail;
     q.head = (uint32_t)(tail + n);
     struct test_item *items = calloc((size_t)n + 1, sizeof *items);
-    int64_t *idx_of = calloc((size_t)n + 1, sizeof *idx_of);
+    char *used = calloc((size_t)ring + 1, 1);
+    if (n > ring) {
+        fprintf(stderr, "%d entries in a ring of %d\n", n, ring);
+        return 5;
+    }
     for (int e = 0; e < n; ++e) {
         uint64_t xa[2];
         int32_t li[3];
         rd(in, xa, sizeof xa);
         rd(in, li, sizeof li);
-        struct rep_queue_item *it = &q.items[(uint32_t)(tail + e) % q.cap];
+        const uint32_t slot = (uint32_t)(tail + e) % q.cap;
+        if (used[slot]++) { /* only a ring whose indices wrap 2^32 can do this: not a rep_queue */
+            fprintf(stderr, "entry %d reuses ring slot %u\n", e, slot);
+            return 5;
+        }
+        struct rep_queue_item *it = &q.items[slot];
         memset(it, 0, sizeof *it);
         it->xid = xa[0];
         it->lid = lid;

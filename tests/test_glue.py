@@ -31,7 +31,8 @@ def _need_exe():
 def write_input(path, *, lid, self_lid, k, m, ring, tail, entries, done, stable, cap, arena=0, parity=None):
     """entries: [(xid, addr, bytes, vnbytes, veto)] at ring indices tail, tail+1, ..."""
     with open(path, "wb") as f:
-        f.write(struct.pack("<9i", lid, self_lid, k, m, ring, tail, len(entries), arena, cap))
+        tail32 = tail - (1 << 32) if tail >= 1 << 31 else tail  # the driver reads it as uint32
+        f.write(struct.pack("<9i", lid, self_lid, k, m, ring, tail32, len(entries), arena, cap))
         f.write(struct.pack("<2Q", done, stable))
         for xid, addr, val, vn, veto in entries:
             f.write(struct.pack("<2Q3i", xid, addr, len(val), vn, veto))
@@ -154,3 +155,48 @@ def test_collect_under_asan_ubsan(tmp_path):
     finally:
         EXE = saved
         os.environ.pop("ASAN_OPTIONS", None)
+
+
+def _collect_model(ents, tail, ring, done, stable, cap):
+    """What the drain loop would process (rep_queue_find per xid, memcached.c:7747):
+    per xid of (done, stable], the first entry in ring order [tail, head) with it."""
+    n = stable - done
+    if n <= 0:
+        return []
+    if n > cap:
+        return -7
+    first = {}
+    for e, ent in enumerate(ents):
+        first.setdefault(ent[0], e)
+    out = []
+    for x in range(done + 1, stable + 1):
+        if x not in first:
+            return -1
+        e = first[x]
+        out.append((e, ents[e][1], len(ents[e][2]), 3))
+    return out
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_collect_random_rings(tmp_path, seed):
+    """Random queues against a model of the reference's per-xid loop: ring sizes 1-64,
+    tails anywhere rep_queue_add leaves them (below twice the ring: it rebases both indices
+    by cap once tail passes cap, rep_queue.c:51-55), xids ascending with gaps and repeats,
+    windows inside, across and beyond the queued xids, scratch caps below and above the
+    window."""
+    _need_exe()
+    rng = np.random.default_rng(1000 + seed)
+    ring = int(rng.integers(1, 65))
+    count = int(rng.integers(0, ring + 1))
+    tail = int(rng.choice([0, rng.integers(0, ring), rng.integers(ring, 2 * ring)]))
+    x, ents = int(rng.integers(0, 50)), []
+    for _ in range(count):
+        x += int(rng.choice([0, 1, 1, 1, 2]))  # repeats and gaps
+        n = int(rng.integers(1, 40))
+        ents.append((x, 16 * int(rng.integers(0, 4096)), rng.integers(0, 256, n, dtype=np.uint8), n, 0))
+    lo = int(rng.integers(0, x + 3))
+    done, stable = lo, lo + int(rng.integers(0, 12))
+    cap = int(rng.integers(0, 16))
+    got = collect(tmp_path, lid=3, self_lid=4, k=3, m=2, ring=ring, tail=tail, entries=ents, done=done,
+                  stable=stable, cap=cap)
+    assert got == _collect_model(ents, tail, ring, done, stable, cap), (ring, tail, done, stable, cap)
