@@ -89,4 +89,11 @@ k)
   # the default line with the other configs' CPU baselines
   run bench_default 400 python -u bench.py
   ;;
+l)
+  # the drain's radix-sorted wave colouring: every drain test, then the drain lines
+  run drain_tests 600 $PYT -m gpu -k "drainer or glue or batched_bindings or registered_host or release_stream" tests
+  run bench_drain 300 python -u bench.py --drain --steps 5 --warmup 2
+  run glue_bench 300 oracle/_ref/glue_drain bench 65536 4098
+  run glue_bench_4k 300 oracle/_ref/glue_drain bench 65536 4096
+  ;;
 esac
