@@ -324,3 +324,20 @@ def test_roofline_traffic_tied_to_the_build(tmp_path, monkeypatch):
     del doc["_build"]
     (prof / "pmc_traffic.json").write_text(json.dumps(doc))
     assert bench.load_traffic("rs32_4k", code_id="00112233aabbccdd") == ((None, None), True)
+
+
+def test_drain_wave_colouring(tmp_path):
+    """The drainer's host-side colouring (cec_drain.inc: the radix address sort and the
+    greedy interval colouring with its no-overlap fast path), spliced from the shipped
+    source into tests/drain_c/waves_main.cpp and run under ASan + UBSan on 3,000 random
+    batches: overlapping updates never share a launch wave, distinct values take one."""
+    src = open(os.path.join(ROOT, "cocytus_amd", "csrc", "cec_drain.inc")).read()
+    a, b = src.index("static void sort_by_addr("), src.index("CEC_API int cec_drainer_apply(")
+    prog = open(os.path.join(ROOT, "tests", "drain_c", "waves_main.cpp")).read()
+    cpp = tmp_path / "waves.cpp"
+    cpp.write_text(prog.replace("// WAVES_FUNCS", src[a:b]))
+    exe = tmp_path / "waves"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-o", str(exe), str(cpp)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr[-2000:]
