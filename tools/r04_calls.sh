@@ -96,4 +96,11 @@ l)
   run glue_bench 300 oracle/_ref/glue_drain bench 65536 4098
   run glue_bench_4k 300 oracle/_ref/glue_drain bench 65536 4096
   ;;
+m)
+  # the final host code: the GPU suite, then ASan + UBSan and TSan (sanitizer builds travel
+  # for this call only)
+  run pytest 900 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread
+  run asan 600 bash tools/asan.sh run
+  run tsan 600 bash tools/tsan.sh run
+  ;;
 esac
