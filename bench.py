@@ -944,6 +944,7 @@ def run_device(args):
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_run": max(1, args.warmup),  # warmups actually run (at least one per measurement)
             "ms_per_step": round(r["ms_per_step"], 4),
             "higher_is_better": True,
             "scaling": "weak",

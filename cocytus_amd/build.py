@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libcocytus_ec.so")
 JERASURE_LINK = os.path.join(HERE, "libJerasure.so")
 SOURCES = [os.path.join(CSRC, "cec_runtime.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("cec_kernels.hpp", "gf256.hpp", "cec_cache.inc", "cec_drain.inc", "cec_recovery.inc", "cec_pool.inc")] + [
+DEPS = SOURCES + [os.path.join(CSRC, f) for f in ("cec_kernels.hpp", "gf256.hpp", "cec_cache.inc", "cec_drain.inc", "cec_recovery.inc", "cec_pool.inc", "cec_hostbatch.inc")] + [
     os.path.join(ROOT, "include", f) for f in ("cocytus_ec.h", "galois.h", "jerasure.h", "reed_sol.h")
 ]
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")

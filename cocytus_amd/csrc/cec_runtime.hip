@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <cerrno>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -455,9 +456,12 @@ static const uint64_t g_wt_max_bytes = [] {
     const uint64_t dflt = uint64_t(512) << 20;
     const char *e = getenv("CEC_WT_MAX_BYTES");
     if (!e || !*e) return dflt;
+    // strtoull alone would take "-1" as 2^64 - 1 and skip leading blanks: a byte count is
+    // digits only (decimal, 0x hex or 0 octal), in range
     char *end = nullptr;
-    const unsigned long long v = strtoull(e, &end, 0);
-    if (!end || *end) {
+    errno = 0;
+    const unsigned long long v = (*e >= '0' && *e <= '9') ? strtoull(e, &end, 0) : 0;
+    if (!(*e >= '0' && *e <= '9') || !end || *end || errno == ERANGE) {
         fprintf(stderr, "libcocytus_ec: CEC_WT_MAX_BYTES=%s is not a byte count; using %llu\n", e,
                 static_cast<unsigned long long>(dflt));
         return dflt;
@@ -1265,6 +1269,7 @@ CEC_API int cec_last_sync(cec_sync_record *out) {
 #include "cec_drain.inc"
 #include "cec_recovery.inc"
 #include "cec_pool.inc"
+#include "cec_hostbatch.inc"
 
 // ============================================================== events / streams
 CEC_API int cec_event_create(void **ev) {
@@ -1323,6 +1328,29 @@ CEC_API int cec_copy(void *dst, const void *src, size_t n, void *stream) {
     int dev;
     if (int r = current_device(&dev)) return r;
     if (n) HIP_TRY(hipMemcpyAsync(dst, src, n, hipMemcpyDefault, static_cast<hipStream_t>(stream)));
+    return CEC_OK;
+}
+
+CEC_API int cec_host_register(void *p, size_t bytes, uint8_t **device_alias) {
+    if (!p || !bytes || !device_alias) return fail(CEC_EINVAL, "cec_host_register: bad args");
+    *device_alias = nullptr;
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterMapped));
+    void *d = nullptr;
+    if (hipError_t e = hipHostGetDevicePointer(&d, p, 0); e != hipSuccess) {
+        (void)hipHostUnregister(p);
+        return fail(CEC_EHIP, "cec_host_register: hipHostGetDevicePointer: %s", hipGetErrorString(e));
+    }
+    *device_alias = static_cast<uint8_t *>(d);
+    return CEC_OK;
+}
+
+CEC_API int cec_host_unregister(void *p) {
+    if (!p) return fail(CEC_EINVAL, "cec_host_unregister: NULL");
+    int dev;
+    if (int r = current_device(&dev)) return r;
+    HIP_TRY(hipHostUnregister(p));
     return CEC_OK;
 }
 

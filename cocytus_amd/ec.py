@@ -72,6 +72,25 @@ class HostUpdate(ctypes.Structure):
     ]
 
 
+class RegionJob(ctypes.Structure):
+    """cec_region_job: one galois_w08_region_multiply call of a host-memory batch."""
+
+    _fields_ = [
+        ("src", ctypes.c_void_p),
+        ("dst", ctypes.c_void_p),
+        ("base", ctypes.c_void_p),
+        ("len", ctypes.c_uint32),
+        ("multby", ctypes.c_int32),
+        ("add", ctypes.c_int32),
+    ]
+
+
+class BatchStats(ctypes.Structure):
+    """cec_batch_stats: the thread's last cec_region_multiply_batch."""
+    _fields_ = [("launches", ctypes.c_int), ("rounds", ctypes.c_int), ("plan_us", ctypes.c_float),
+                ("pack_us", ctypes.c_float), ("gpu_us", ctypes.c_float), ("unpack_us", ctypes.c_float)]
+
+
 class CacheInfo(ctypes.Structure):
     """cec_cache_info: the coefficient-table cache and the idle-buffer caches."""
 
@@ -131,6 +150,9 @@ _SIGS = {
     "cec_drainer_destroy": ([_vp], _i),
     "cec_drainer_apply": ([_vp, ctypes.POINTER(HostUpdate), _i, _vp, _vp], _i),
     "cec_drainer_last_launches": ([_vp], _i),
+    "cec_drainer_validate": ([_vp, ctypes.POINTER(HostUpdate), _i], _i),
+    "cec_region_multiply_batch": ([ctypes.POINTER(RegionJob), _i, _vp], _i),
+    "cec_region_multiply_batch_stats": ([ctypes.POINTER(BatchStats)], _i),
     "cec_drainer_staging": ([_vp, ctypes.POINTER(ctypes.c_size_t)], ctypes.POINTER(ctypes.c_uint8)),
     "cec_recovery_create": ([ctypes.POINTER(_vp), _i, _i, _ip, _i, _u32, _i, _i, _vp, _vp], _i),
     "cec_recovery_destroy": ([_vp], _i),
@@ -164,6 +186,9 @@ _SIGS = {
     "cec_event_record": ([_vp, _vp], _i),
     "cec_event_elapsed_ms": ([_vp, _vp, ctypes.POINTER(ctypes.c_float)], _i),
     "cec_stream_synchronize": ([_vp], _i),
+    "cec_host_register": ([_vp, ctypes.c_size_t, ctypes.POINTER(_vp)], _i),
+    "cec_host_unregister": ([_vp], _i),
+    "cec_copy": ([_vp, _vp, ctypes.c_size_t, _vp], _i),
     "cec_device_count": ([ctypes.POINTER(_i)], _i),
     "cec_set_device": ([_i], _i),
     "cec_stream_create": ([ctypes.POINTER(_vp)], _i),
@@ -277,6 +302,8 @@ def _ptr(x) -> int:
         return 0
     if isinstance(x, int):
         return x
+    if hasattr(x, "__index__") and not hasattr(x, "data_ptr"):  # numpy integers
+        return x.__index__()
     if hasattr(x, "data_ptr"):
         return int(x.data_ptr())
     raise TypeError(f"cannot take a device pointer of {type(x)!r}")
@@ -752,6 +779,24 @@ def galois_w08_region_multiply(region, multby: int, nbytes: int, r2, add: int) -
     numpy arrays) -- host buffers are passed by address.
     """
     lib().galois_w08_region_multiply(_host_or_dev(region), multby, nbytes, _host_or_dev(r2), add)
+
+
+def region_multiply_batch(jobs, stream=None) -> tuple[int, int]:
+    """cec_region_multiply_batch over host buffers.  jobs: (src, dst, base, len, multby,
+    add) with src / dst / base as host addresses (int), numpy arrays, bytearrays or None.
+    Returns (kernel launches, staging rounds) of the call."""
+    arr = (RegionJob * len(jobs))()
+    for i, (src, dst, base, n, c, add) in enumerate(jobs):
+        arr[i] = RegionJob(_host_or_dev(src), _host_or_dev(dst), _host_or_dev(base), n, c, add)
+    _check(lib().cec_region_multiply_batch(arr, len(jobs), _stream(stream)))
+    st = batch_stats()
+    return st["launches"], st["rounds"]
+
+
+def batch_stats() -> dict:
+    st = BatchStats()
+    _check(lib().cec_region_multiply_batch_stats(ctypes.byref(st)))
+    return {f: getattr(st, f) for f, _ in BatchStats._fields_}
 
 
 def _host_or_dev(x):

@@ -233,6 +233,12 @@ int cec_drainer_release_stream(cec_drainer *d, void *stream);   /* LIFETIME RULE
 int cec_drainer_apply(cec_drainer *d, const cec_host_update *updates, int n,
                       uint8_t *parity, void *stream);
 
+/* The checks cec_drainer_apply makes on its updates before it touches anything (src_lid
+ * < k, buf non-NULL when len > 0, len <= half the staging area), on the host only: CEC_OK
+ * or CEC_EINVAL.  A caller with side effects per update (the server's recovery fold) runs
+ * it first, so that an update the apply would refuse is refused before any of them. */
+int cec_drainer_validate(const cec_drainer *d, const cec_host_update *updates, int n);
+
 /* Launches the last cec_drainer_apply needed (>= 1 when n > 0: overlap waves x rounds). */
 int cec_drainer_last_launches(const cec_drainer *d);
 
@@ -242,6 +248,44 @@ int cec_drainer_last_launches(const cec_drainer *d);
  * cec_drainer_apply call points into it, the call skips the pack copy: one H2D of the
  * used span, then the fold.  The caller must not write the area during an apply. */
 uint8_t *cec_drainer_staging(cec_drainer *d, size_t *capacity);
+
+/* ---- galois_w08_region_multiply, batched, over host memory ----
+ * The unchanged server keeps its recovery state in host memory -- one malloc'd 4 KiB
+ * buffer per recovery unit (recovery.c:79), the parity arena ecmem (recovery.c:81),
+ * malloc'd peer replies and diffs, calloc'd solve outputs (memcached.c:7913) -- and calls
+ * galois_w08_region_multiply once per unit (recovery.c:91, 123; memcached.c:7918).  This
+ * runs a whole list of such calls as one staged pass (one kernel launch per overlap wave):
+ *
+ *   add = 0              : dst  = multby * src
+ *   add = 1, base = NULL : dst ^= multby * src      (galois_w08_region_multiply(src, multby, len, dst, 1))
+ *   add = 1, base != NULL: dst  = base ^ multby * src  (the first-touch copy of recovery.c:79-82,
+ *                                                      then the fold of :91, fused)
+ *
+ * The bytes equal the calls run one by one in job order: jobs whose dst ranges overlap are
+ * applied in separate launches (in job order when one of them writes; XOR accumulation
+ * commutes).  A src or base range must not overlap any job's dst (CEC_EOVERLAP; base ==
+ * dst is the in-place add).  Every pointer is HOST memory (pageable, pinned or registered;
+ * device-resident state uses the device ops above).  Synchronous: on return every dst
+ * holds its bytes.  Lengths and alignments are arbitrary. */
+typedef struct cec_region_job {
+    const void *src;    /* region (read) */
+    void *dst;          /* r2 (written) */
+    const void *base;   /* see above; NULL for the plain call */
+    uint32_t len;       /* nbytes */
+    int32_t multby;     /* 0..255 */
+    int32_t add;        /* 0 or 1 */
+} cec_region_job;
+
+int cec_region_multiply_batch(const cec_region_job *jobs, int n, void *stream);
+/* Diagnostics of the calling thread's last batch: kernel launches (overlap waves x
+ * rounds), staging rounds, and host wall time in microseconds spent planning (clusters,
+ * waves, patterns), packing the inputs into the staging, in the GPU pass (launch to
+ * completion) and unpacking the results. */
+typedef struct cec_batch_stats {
+    int launches, rounds;
+    float plan_us, pack_us, gpu_us, unpack_us;
+} cec_batch_stats;
+int cec_region_multiply_batch_stats(cec_batch_stats *out);
 
 /* ---- online recovery over 4 KiB unit ranges ----
  * One recovery request on a participating parity (recovery_queue_item,
@@ -419,6 +463,13 @@ int cec_stream_destroy(void *stream);
 /* Async copy between any host / device buffers (arena bytes to and from the server's
  * buffers); complete after cec_stream_synchronize(stream). */
 int cec_copy(void *dst, const void *src, size_t n, void *stream);
+/* A host arena the server keeps in its own memory (ecmem: mmap'd, ecmem.h:36-42) made
+ * reachable by the kernels: page-locked and mapped once
+ * (hipHostRegister), *device_alias = its address for the device ops (cec_encode,
+ * cec_drainer_apply, ...; results are complete for the host after the op's stream
+ * synchronises, or on return of the synchronous calls).  Unregister before freeing it. */
+int cec_host_register(void *p, size_t bytes, uint8_t **device_alias);
+int cec_host_unregister(void *p);
 
 #ifdef __cplusplus
 }

@@ -46,17 +46,33 @@ int cocytus_drain_gf(const struct rep_queue *q, int lid, uint64_t done_xid, uint
     if (!drainer || !parity) return CEC_EINVAL;
     const int n = cocytus_drain_collect(q, lid, done_xid, stable_xid, hooks, scratch, cap);
     if (n <= 0) return n;
+    /* the folds below have side effects: refuse a window the apply would refuse first */
+    int rc = cec_drainer_validate(drainer, scratch, n);
+    if (rc) return rc;
     /* process_rep_command's order: the recovery fold decides, per xid, whether the
      * parity arena takes the diff (memcached.c:7758-7767) */
     int m = 0;
-    for (int i = 0; i < n; ++i) {
-        cec_host_update u = scratch[i];
-        if (hooks->try_update &&
-            !hooks->try_update(lid, u.addr, (char *)(uintptr_t)u.buf, u.len, hooks->ctx))
-            continue;
-        scratch[m++] = u;
+    if (hooks->try_update_batch) {
+        int *need = malloc(sizeof(int) * (size_t)n);
+        if (!need) return CEC_ENOMEM;
+        rc = hooks->try_update_batch(scratch, n, need, hooks->ctx);
+        if (rc < 0) {
+            free(need);
+            return rc;
+        }
+        for (int i = 0; i < n; ++i)
+            if (need[i]) scratch[m++] = scratch[i];
+        free(need);
+    } else {
+        for (int i = 0; i < n; ++i) {
+            cec_host_update u = scratch[i];
+            if (hooks->try_update &&
+                !hooks->try_update(lid, u.addr, (char *)(uintptr_t)u.buf, u.len, hooks->ctx))
+                continue;
+            scratch[m++] = u;
+        }
     }
     if (m == 0) return 0;
-    const int rc = cec_drainer_apply(drainer, scratch, m, parity, stream);
+    rc = cec_drainer_apply(drainer, scratch, m, parity, stream);
     return rc < 0 ? rc : m;
 }

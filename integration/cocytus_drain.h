@@ -47,6 +47,10 @@ typedef struct cocytus_drain_hooks {
      * applied. */
     int (*try_update)(int lid, uint64_t addr, char *buf, uint32_t nbytes, void *ctx);
     void *ctx;
+    /* The same fold for the whole window at once (cocytus_recovery.h: cocytus_fold_hook,
+     * one batch for every unit piece of every update): need[i] = try_update's answer for
+     * u[i]; returns >= 0, or a negative cec_status.  Used instead of try_update when set. */
+    int (*try_update_batch)(const cec_host_update *u, int n, int *need, void *ctx);
 } cocytus_drain_hooks;
 
 /* The entries of q with done_xid < xid <= stable_xid, in xid order, as cec_host_updates
@@ -57,11 +61,16 @@ typedef struct cocytus_drain_hooks {
 int cocytus_drain_collect(const struct rep_queue *q, int lid, uint64_t done_xid, uint64_t stable_xid,
                           const cocytus_drain_hooks *hooks, cec_host_update *out, int cap);
 
-/* The GF half of the drain loop above, batched: collect, ask hooks->try_update about each
- * entry in xid order, then ONE cec_drainer_apply of the diffs it let through into the
- * parity arena (device; synchronous, like the loop).  `scratch`: cap cec_host_updates.
- * Returns the number of diffs applied (>= 0) or a negative cec_status.  The caller then
- * runs, per xid, the rest of process_rep_command (store the item, mark done, flush). */
+/* The GF half of the drain loop above, batched: collect, check every entry as
+ * cec_drainer_apply will (cec_drainer_validate: nothing is folded for a window the apply
+ * would refuse), ask the recovery fold about each entry in xid order (hooks->try_update,
+ * or hooks->try_update_batch once), then ONE cec_drainer_apply of the diffs it let through
+ * into the parity arena (device or registered host memory; synchronous, like the loop).
+ * `scratch`: cap cec_host_updates.  Returns the number of diffs applied (>= 0) or a
+ * negative cec_status.  A failure after the folds ran (the apply's HIP error) leaves the
+ * recovery units ahead of the arena: the recovery state is inconsistent and the process
+ * must stop (retrying the window would fold its diffs twice).  The caller then runs, per
+ * xid, the rest of process_rep_command (store the item, mark done, flush). */
 int cocytus_drain_gf(const struct rep_queue *q, int lid, uint64_t done_xid, uint64_t stable_xid,
                      const cocytus_drain_hooks *hooks, cec_drainer *drainer, uint8_t *parity,
                      void *stream, cec_host_update *scratch, int cap);

@@ -7,11 +7,17 @@
  *                               collected update "entry addr len lid", or "rc N"
  *   drain_main apply IN OUT     GPU: cocytus_drain_gf into a device parity arena that
  *                               starts from IN's parity bytes; OUT = the arena afterwards
- *   drain_main bench N SIZE [MB] GPU: N queued SIZE-byte diffs of one peer drained (a) by
- *                               cocytus_drain_gf into a device arena, (b) by the unchanged
+ *   drain_main bench N SIZE [MB [PLACE]]
+ *                               GPU: N queued SIZE-byte diffs of one peer drained (a) by
+ *                               cocytus_drain_gf into the parity arena, (b) by the unchanged
  *                               loop through the drop-in (one galois_w08_region_multiply
- *                               per xid into a host ecmem, memcached.c:7764); one JSON line;
- *                               MB: the drainer's staging (default 64 MiB)
+ *                               per xid into a pageable host ecmem, memcached.c:7764), (c) by
+ *                               the same loop on the restated CPU region multiply (oracle,
+ *                               SIMD, one thread: the reference's GF-Complete path, restated);
+ *                               one JSON line.  MB: the drainer's staging (default 64 MiB).
+ *                               PLACE: where (a)'s arena lives -- "device" (HBM, default) or
+ *                               "host" (the unchanged server's ecmem: host memory registered
+ *                               with cec_host_register, the kernels reach it over PCIe)
  *
  * IN (little-endian): int32 lid, self_lid, k, m, ring_cap, tail, n_entries, arena_bytes,
  * cap; uint64 done_xid, stable_xid; n_entries x {uint64 xid, uint64 addr, int32 len,
@@ -29,6 +35,7 @@
 #include <reed_sol.h>
 
 #include "cocytus_drain.h"
+#include "gf8_ref.h" /* oracle: the restated CPU region multiply (test infrastructure, baseline (c)) */
 #include "rep_queue.h"
 
 struct test_item { /* what item_nbytes reads: the test's own value record */
@@ -41,7 +48,8 @@ static uint32_t item_nbytes(void *item, void *ctx) {
     return ((struct test_item *)item)->nbytes;
 }
 
-static int vetoes; /* try_update calls that kept a diff out of the arena */
+static int vetoes;     /* try_update calls that kept a diff out of the arena */
+static int hook_calls; /* try_update calls */
 
 static int try_update(int lid, uint64_t addr, char *buf, uint32_t nbytes, void *ctx) {
     /* the test's recovery fold: the entry's veto flag, found by its buffer */
@@ -49,6 +57,7 @@ static int try_update(int lid, uint64_t addr, char *buf, uint32_t nbytes, void *
     (void)lid; (void)addr; (void)nbytes;
     int veto = items[((int32_t *)buf)[-1]].veto; /* entry index stored before the bytes */
     vetoes += veto;
+    hook_calls++;
     return !veto;
 }
 
@@ -71,7 +80,7 @@ static uint32_t plain_nbytes(void *item, void *ctx) {
 }
 
 /* Server-level drain rate: the glue against the unchanged per-xid loop on the shim. */
-static int bench(int n, int size, int staging_mb) {
+static int bench(int n, int size, int staging_mb, int host_arena) {
     const int K = 3, M = 2, lid = 1, self = K + 1;
     const size_t arena = (size_t)n * (size_t)size;
     struct rep_queue q;
@@ -109,14 +118,21 @@ static int bench(int n, int size, int staging_mb) {
     if (cec_device_check() != CEC_OK) return 2;
     int *matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
     uint8_t *parity;
-    void *slab;
+    void *slab = NULL;
+    uint8_t *host = NULL;
     cec_drainer *dr;
     uint8_t *ecmem = calloc(arena, 1); /* the host ecmem of the unchanged loop; zeros */
-    if (cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, ecmem, arena, NULL) ||
-        cec_stream_synchronize(NULL) || cec_drainer_create(&dr, K, M, matrix, self, (size_t)staging_mb << 20))
+    uint8_t *cpu_ecmem = calloc(arena, 1);
+    if (host_arena) { /* the server's own host ecmem, registered once */
+        if (posix_memalign((void **)&host, 4096, arena) || cec_host_register(memset(host, 0, arena), arena, &parity))
+            return 2;
+    } else if (cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, ecmem, arena, NULL) ||
+               cec_stream_synchronize(NULL)) {
         return 2;
+    }
+    if (cec_drainer_create(&dr, K, M, matrix, self, (size_t)staging_mb << 20)) return 2;
     cec_host_update *scratch = calloc((size_t)n, sizeof *scratch);
-    cocytus_drain_hooks hooks = {plain_nbytes, NULL, NULL};
+    cocytus_drain_hooks hooks = {.item_nbytes = plain_nbytes};
     double best = 1e30, t_sum = 0;
     const int reps = 4; /* + one warm-up: 5 drains, an odd count, so the arena holds each diff once */
     for (int r = 0; r < reps + 1; ++r) {
@@ -138,30 +154,50 @@ static int bench(int n, int size, int staging_mb) {
     for (int e = 0; e < n; ++e)
         galois_w08_region_multiply(q.items[e].vbuf, c, size, (char *)ecmem + q.items[e].addr, 1);
     const double t_loop = now_s() - t1;
-    /* both paths applied every diff once: the same bytes, and not all zero */
+    /* the same loop on the restated CPU path: GF-Complete's split-table SIMD multiply, one
+     * thread, into a pageable ecmem (5 passes, like the glue's: each diff applied once) */
+    double t_cpu = 1e30;
+    for (int r = 0; r < 5; ++r) {
+        const double t2 = now_s();
+        for (int e = 0; e < n; ++e)
+            ref_region_multiply_simd((const uint8_t *)q.items[e].vbuf, c, size, cpu_ecmem + q.items[e].addr);
+        const double t = now_s() - t2;
+        if (t < t_cpu) t_cpu = t;
+    }
+    /* every path applied every diff once: the same bytes, and not all zero */
     uint8_t *dev_copy = malloc(arena);
     if (cec_copy(dev_copy, parity, arena, NULL) || cec_stream_synchronize(NULL)) return 2;
     int nonzero = 0;
     for (size_t i = 0; i < arena && !nonzero; ++i) nonzero = ecmem[i] != 0;
-    const int ok = nonzero && memcmp(dev_copy, ecmem, arena) == 0;
+    const int ok = nonzero && memcmp(dev_copy, ecmem, arena) == 0 && memcmp(cpu_ecmem, ecmem, arena) == 0 &&
+                   (!host || memcmp(host, ecmem, arena) == 0);
     const double gib = (double)arena / (double)(1u << 30);
     printf("{\"path\": \"server drain loop over the real rep_queue: %d queued %d-byte diffs of one peer\", "
-           "\"staging_MiB\": %d, "
+           "\"arena\": \"%s\", \"staging_MiB\": %d, "
            "\"glue_GiBps\": %.2f, \"glue_runs\": %d, \"glue_ms_mean\": %.3f, \"glue_ms_best\": %.3f, "
            "\"dropin_loop_GiBps\": %.3f, \"dropin_loop_ms\": %.1f, \"dropin_us_per_xid\": %.2f, "
-           "\"speedup\": %.1f, \"launches\": %d, \"verified\": %s}\n",
-           n, size, staging_mb, gib / (t_sum / reps), reps, 1e3 * t_sum / reps, 1e3 * best, gib / t_loop, 1e3 * t_loop,
-           1e6 * t_loop / n, t_loop / (t_sum / reps), cec_drainer_last_launches(dr), ok ? "true" : "false");
+           "\"cpu_restated_1thread_GiBps\": %.2f, \"cpu_restated_ms_best\": %.3f, "
+           "\"speedup_vs_dropin\": %.1f, \"speedup_vs_cpu_1thread\": %.2f, \"launches\": %d, \"verified\": %s}\n",
+           n, size, host ? "host ecmem, registered (cec_host_register), reached over PCIe" : "device (HBM)",
+           staging_mb, gib / (t_sum / reps), reps, 1e3 * t_sum / reps, 1e3 * best, gib / t_loop, 1e3 * t_loop,
+           1e6 * t_loop / n, gib / t_cpu, 1e3 * t_cpu, t_loop / (t_sum / reps), t_cpu / (t_sum / reps),
+           cec_drainer_last_launches(dr), ok ? "true" : "false");
     cec_drainer_destroy(dr);
-    cec_arenas_free(slab);
+    if (slab) cec_arenas_free(slab);
+    if (host) cec_host_unregister(host);
     return ok ? 0 : 4;
 }
 
 int main(int argc, char **argv) {
-    if ((argc == 4 || argc == 5) && !strcmp(argv[1], "bench"))
-        return bench(atoi(argv[2]), atoi(argv[3]), argc == 5 ? atoi(argv[4]) : 64);
+    if (argc >= 4 && argc <= 6 && !strcmp(argv[1], "bench"))
+        return bench(atoi(argv[2]), atoi(argv[3]), argc >= 5 ? atoi(argv[4]) : 64,
+                     argc == 6 && !strcmp(argv[5], "host"));
     if (argc != 4) return 1;
-    const int apply = !strcmp(argv[1], "apply");
+    /* apply: into a device arena; apply_host: into a registered host arena (the unchanged
+     * server's ecmem); apply4k: a drainer with 4 KiB of staging per half, so a window with a
+     * larger diff is refused -- before any fold hook runs (cec_drainer_validate) */
+    const int host_mode = !strcmp(argv[1], "apply_host"), small = !strcmp(argv[1], "apply4k");
+    const int apply = !strcmp(argv[1], "apply") || host_mode || small;
     FILE *in = fopen(argv[2], "rb");
     if (!in) return 1;
     int32_t h[9];
@@ -209,7 +245,7 @@ int main(int argc, char **argv) {
         it->vbuf = (char *)(blk + 1);
         rd(in, it->vbuf, items[e].nbytes);
     }
-    cocytus_drain_hooks hooks = {item_nbytes, try_update, items};
+    cocytus_drain_hooks hooks = {.item_nbytes = item_nbytes, .try_update = try_update, .ctx = items};
     cec_host_update *scratch = calloc((size_t)cap + 1, sizeof *scratch);
     FILE *out = fopen(argv[3], apply ? "wb" : "w");
     if (!out) return 1;
@@ -236,24 +272,41 @@ int main(int argc, char **argv) {
     }
     int *matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
     uint8_t *parity;
-    void *slab;
+    void *slab = NULL;
+    uint8_t *reg = NULL;
     cec_drainer *dr;
-    if (cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, host, arena, NULL) ||
-        cec_stream_synchronize(NULL) || cec_drainer_create(&dr, K, M, matrix, self, 1 << 20)) {
+    int setup;
+    if (host_mode) {
+        setup = posix_memalign((void **)&reg, 4096, arena) || !memcpy(reg, host, arena) ||
+                cec_host_register(reg, arena, &parity);
+    } else {
+        setup = cec_arenas_alloc(1, arena, &parity, &slab) || cec_copy(parity, host, arena, NULL) ||
+                cec_stream_synchronize(NULL);
+    }
+    if (setup || cec_drainer_create(&dr, K, M, matrix, self, small ? 4096 : 1 << 20)) {
         fprintf(stderr, "setup: %s\n", cec_last_error());
         return 2;
     }
     const int applied = cocytus_drain_gf(&q, lid, x[0], x[1], &hooks, dr, parity, NULL, scratch, cap);
+    if (small) { /* the refusal: no hook ran, the arena is untouched */
+        if (cec_copy(host, parity, arena, NULL) || cec_stream_synchronize(NULL)) return 2;
+        fwrite(host, 1, arena, out);
+        fclose(out);
+        printf("rc %d hooks %d\n", applied, hook_calls);
+        return 0;
+    }
     if (applied < 0) {
         fprintf(stderr, "cocytus_drain_gf: %d %s\n", applied, cec_last_error());
         return 2;
     }
-    if (cec_copy(host, parity, arena, NULL) || cec_stream_synchronize(NULL)) return 2;
+    if (reg) memcpy(host, reg, arena); /* the host arena itself: complete when the drain returned */
+    else if (cec_copy(host, parity, arena, NULL) || cec_stream_synchronize(NULL)) return 2;
     fwrite(host, 1, arena, out);
     fclose(out);
     printf("applied %d vetoed %d launches %d\n", applied, vetoes, cec_drainer_last_launches(dr));
     cec_drainer_destroy(dr);
-    cec_arenas_free(slab);
+    if (slab) cec_arenas_free(slab);
+    if (reg) cec_host_unregister(reg);
     free(matrix);
     return 0;
 }

@@ -1,0 +1,222 @@
+/*
+ * tests/glue/recovery_bench.c -- the recovery glue (integration/cocytus_recovery.c) against
+ * the unchanged server's per-unit code, at server level, over the server's own types
+ * (compiled against the reference's recovery.h / ecmem.h where they lie).
+ *
+ *   recovery_bench [REPS]      one JSON line per shape:
+ *
+ *   range_1MiB  one recovery request over 256 units (1 MiB), RS(3,2), this parity P1 the
+ *               leader of a single loss (D1 lost; mask P1 + D0 + D2, start_recovery's):
+ *               two data peers' replies (recovery_recover_units, recovery.c:61-96), then
+ *               the leader solve (complete_recovery_bottom_half, memcached.c:7842-7922).
+ *   idle_85     the idle recoverer's 85 single-unit requests in flight (idle_event_handler,
+ *               memcached.c:5712-5734; TOO_MANY_RECOVERY, const.h:27) at scattered units:
+ *               2 replies each, then 85 leader solves.
+ *
+ * Paths, all from the same inputs, outputs compared byte for byte:
+ *   glue        cocytus_recover_units_gf x peers + cocytus_recovery_solve_gf (range), or
+ *               every reply and solve deferred and ONE cocytus_recovery_flush (idle);
+ *   dropin      the reference's loops as the unchanged server runs them on the shim: one
+ *               synchronous galois_w08_region_multiply per unit (and per solve term);
+ *   cpu         the same loops on the restated CPU region multiply (oracle: GF-Complete's
+ *               split-table SIMD, one thread) -- the reference's own CPU path, restated.
+ * The recovery state and the arena are host memory in every path (the unchanged server's).
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <cocytus_ec.h>
+
+#include "cocytus_recovery.h"
+#include "gf8_ref.h" /* oracle: the restated CPU region multiply (baseline only) */
+
+#define K 3
+#define M 2
+#define SELF 4 /* P1 */
+#define U ((size_t)UNITSIZE)
+
+typedef void (*mul_fn)(char *region, int multby, int nbytes, char *r2);
+
+static void mul_dropin(char *region, int c, int n, char *r2) { galois_w08_region_multiply(region, c, n, r2, 1); }
+static void mul_cpu(char *region, int c, int n, char *r2) {
+    ref_region_multiply_simd((const uint8_t *)region, c, n, (uint8_t *)r2);
+}
+
+static int *matrix;
+#define MAT(x, y) matrix[(x) * K + (y)]
+
+/* recovery_recover_units (recovery.c:61-96), per unit */
+static void ref_recover(struct recovery *r, struct ecmem *ecm, int peer, int ub, int ue, char *data, mul_fn mul) {
+    for (int i = ub; i <= ue; ++i, data += U) {
+        struct recovery_unit *u = &r->units[i];
+        if (!(u->flags & (1u << 30))) {
+            u->data = malloc(U);
+            memcpy(u->data, ecmem_get(ecm, (uint64_t)i * U), U);
+            u->flags |= (1u << 30) | (1u << SELF);
+        }
+        u->flags |= 1u << peer;
+        mul(data, MAT(SELF, peer), (int)U, u->data);
+    }
+}
+
+/* complete_recovery_bottom_half's arithmetic (memcached.c:7842-7922) for a single loss led
+ * by this parity: buf = the units copied out, data = calloc, data ^= inv * buf */
+static char *ref_solve(struct recovery *r, int ub, int ue, int inv, mul_fn mul) {
+    const size_t nbuf = (size_t)(ue - ub + 1) * U;
+    char *buf = malloc(nbuf), *p = buf;
+    for (int i = ub; i <= ue; ++i, p += U) memcpy(p, r->units[i].data, U);
+    char *out = calloc(1, nbuf);
+    mul(buf, inv, (int)nbuf, out);
+    free(buf);
+    return out;
+}
+
+static void reset(struct recovery *r, int nunits) {
+    for (int i = 0; i < nunits; ++i) {
+        free(r->units[i].data);
+        r->units[i].data = NULL;
+        r->units[i].flags = 0;
+    }
+}
+
+static double now_s(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec + 1e-9 * (double)t.tv_nsec;
+}
+
+static int cmp_d(const void *a, const void *b) {
+    const double x = *(const double *)a, y = *(const double *)b;
+    return x < y ? -1 : x > y;
+}
+
+static void fill(char *p, size_t n, uint64_t seed) {
+    for (size_t i = 0; i < n; i += 8) {
+        seed ^= seed << 13, seed ^= seed >> 7, seed ^= seed << 17;
+        memcpy(p + i, &seed, n - i >= 8 ? 8 : n - i);
+    }
+}
+
+/* One shape: nreq requests of `units` units each at unit starts[q]. */
+static int shape(const char *name, int nreq, int units, const int *starts, int reps, int nunits, struct ecmem *ecm,
+                 cocytus_rglue *g) {
+    const int peers[2] = {0, 2}, lost = 1;
+    const uint32_t mask = (1u << SELF) | (1u << 0) | (1u << 2);
+    const int inv = galois_single_divide(1, MAT(SELF, lost), 8);
+    const size_t nbuf = (size_t)units * U;
+    struct recovery r;
+    memset(&r, 0, sizeof r);
+    r.units = calloc((size_t)nunits, sizeof *r.units);
+    char **reply = malloc(sizeof(char *) * (size_t)(2 * nreq)); /* c->vbuf of each reply */
+    for (int x = 0; x < 2 * nreq; ++x) {
+        reply[x] = malloc(nbuf);
+        fill(reply[x], nbuf, 0x1234567ull + (uint64_t)x);
+    }
+    char **out[3];
+    for (int p = 0; p < 3; ++p) out[p] = calloc((size_t)nreq, sizeof(char *));
+    double t[3][64];
+    struct recovery_queue_item *it = calloc((size_t)nreq, sizeof *it);
+    for (int q = 0; q < nreq; ++q) {
+        it[q].unit_begin = starts[q];
+        it[q].unit_end = starts[q] + units - 1;
+        it[q].mask = mask;
+    }
+    for (int path = 0; path < 3; ++path) {
+        for (int rep = 0; rep <= reps; ++rep) { /* rep 0: warm-up */
+            reset(&r, nunits);
+            for (int q = 0; q < nreq; ++q) free(out[path][q]);
+            const double t0 = now_s();
+            if (path == 0) {
+                for (int q = 0; q < nreq; ++q)
+                    for (int p = 0; p < 2; ++p) {
+                        const int rc = nreq == 1 ? cocytus_recover_units_gf(g, &r, ecm, peers[p], it[q].unit_begin,
+                                                                            it[q].unit_end, reply[2 * q + p])
+                                                 : cocytus_recover_units_defer(g, &r, ecm, peers[p], it[q].unit_begin,
+                                                                               it[q].unit_end, reply[2 * q + p], 0);
+                        if (rc) return fprintf(stderr, "recover: %d %s\n", rc, cec_last_error()), 2;
+                    }
+                for (int q = 0; q < nreq; ++q) {
+                    char *data[M];
+                    int n = 0;
+                    const int rc = nreq == 1 ? cocytus_recovery_solve_gf(g, &r, &it[q], data, &n)
+                                             : cocytus_recovery_solve_defer(g, &r, &it[q], data, &n);
+                    if (rc || n != 1) return fprintf(stderr, "solve: %d %s\n", rc, cec_last_error()), 2;
+                    out[0][q] = data[0];
+                }
+                if (nreq > 1 && cocytus_recovery_flush(g) != 3 * nreq)
+                    return fprintf(stderr, "flush: %s\n", cec_last_error()), 2;
+            } else {
+                const mul_fn mul = path == 1 ? mul_dropin : mul_cpu;
+                for (int q = 0; q < nreq; ++q)
+                    for (int p = 0; p < 2; ++p)
+                        ref_recover(&r, ecm, peers[p], it[q].unit_begin, it[q].unit_end, reply[2 * q + p], mul);
+                for (int q = 0; q < nreq; ++q) out[path][q] = ref_solve(&r, it[q].unit_begin, it[q].unit_end, inv, mul);
+            }
+            if (rep) t[path][rep - 1] = now_s() - t0;
+        }
+        qsort(t[path], (size_t)reps, sizeof(double), cmp_d);
+    }
+    int same = 1;
+    for (int q = 0; q < nreq; ++q)
+        same &= !memcmp(out[0][q], out[1][q], nbuf) && !memcmp(out[0][q], out[2][q], nbuf);
+    /* payload: the replies folded + the bytes rebuilt */
+    const double bytes = (double)nreq * (double)nbuf * 3.0, gib = bytes / (double)(1u << 30);
+    const double med[3] = {t[0][reps / 2], t[1][reps / 2], t[2][reps / 2]};
+    cec_batch_stats st;
+    cec_region_multiply_batch_stats(&st);
+    printf("{\"shape\": \"%s\", \"requests\": %d, \"units_per_request\": %d, \"code\": \"RS(3,2), leader P1, D1 lost\", "
+           "\"payload_MiB\": %.3f, \"glue_us\": %.1f, \"glue_GiBps\": %.3f, \"dropin_loop_us\": %.1f, "
+           "\"dropin_loop_GiBps\": %.3f, \"cpu_restated_1thread_us\": %.1f, \"cpu_restated_1thread_GiBps\": %.3f, "
+           "\"glue_vs_dropin\": %.1f, \"glue_vs_cpu_1thread\": %.2f, \"reps\": %d, "
+           "\"last_batch\": {\"launches\": %d, \"pack_us\": %.1f, \"gpu_us\": %.1f, \"unpack_us\": %.1f}, "
+           "\"verified\": %s}\n",
+           name, nreq, units, bytes / (1 << 20), 1e6 * med[0], gib / med[0], 1e6 * med[1], gib / med[1], 1e6 * med[2],
+           gib / med[2], med[1] / med[0], med[2] / med[0], reps, st.launches, st.pack_us, st.gpu_us, st.unpack_us,
+           same ? "true" : "false");
+    reset(&r, nunits);
+    for (int p = 0; p < 3; ++p) {
+        for (int q = 0; q < nreq; ++q) free(out[p][q]);
+        free(out[p]);
+    }
+    for (int x = 0; x < 2 * nreq; ++x) free(reply[x]);
+    free(reply);
+    free(it);
+    free(r.units);
+    return same ? 0 : 4;
+}
+
+int main(int argc, char **argv) {
+    const int reps = argc > 1 ? atoi(argv[1]) : 15;
+    if (reps < 1 || reps > 64) return 1;
+    if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
+    matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
+    const int nunits = 8192; /* a 32 MiB parity arena, host memory (the server's ecmem) */
+    struct ecmem ecm;
+    memset(&ecm, 0, sizeof ecm);
+    ecm.size = (uint64_t)nunits * U;
+    ecm.mem = malloc(ecm.size);
+    fill(ecm.mem, ecm.size, 99);
+    cocytus_rglue *g;
+    if (cocytus_rglue_create(&g, K, M, matrix, SELF, NULL)) return 2;
+    int start = 100;
+    int rc = shape("range_1MiB", 1, 256, &start, reps, nunits, &ecm, g);
+    int starts[85];
+    uint64_t s = 77;
+    for (int q = 0; q < 85; ++q) { /* distinct scattered units */
+        int ok;
+        do {
+            s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+            starts[q] = 512 + (int)(s % (uint64_t)(nunits - 512));
+            ok = 1;
+            for (int x = 0; x < q; ++x) ok &= starts[x] != starts[q];
+        } while (!ok);
+    }
+    rc |= shape("idle_85", 85, 1, starts, reps, nunits, &ecm, g);
+    cocytus_rglue_destroy(g);
+    free(ecm.mem);
+    free(matrix);
+    return rc;
+}

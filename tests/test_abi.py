@@ -291,6 +291,12 @@ def test_store_policy_environment(lib):
     assert got == ("auto", 512 << 20) and "CEC_STORE_POLICY=WT" in err
     got, err = _policy_in_child({"CEC_WT_MAX_BYTES": "lots"})
     assert got == ("auto", 512 << 20) and "CEC_WT_MAX_BYTES=lots" in err
+    # strtoull would read "-1" as 2^64 - 1 (write-through for every launch) and skip blanks;
+    # neither is a byte count, nor is a value past 2^64 - 1
+    for bad in ("-1", " 4096", "+4096", "99999999999999999999999"):
+        got, err = _policy_in_child({"CEC_WT_MAX_BYTES": bad})
+        assert got == ("auto", 512 << 20) and "CEC_WT_MAX_BYTES=" in err, bad
+    assert _policy_in_child({"CEC_WT_MAX_BYTES": "0x1000"})[0] == ("auto", 4096)
 
 
 @pytest.mark.skipif(not os.path.exists(LLVM_OBJDUMP), reason="llvm-objdump not in this image")

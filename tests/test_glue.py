@@ -94,6 +94,67 @@ def test_collect_refuses_gaps_and_overflow(tmp_path):
     assert [(a, n) for _, a, n, _ in got] == [(16, 8), (32, 8), (64, 8)]
 
 
+def _drain_case(rng, count=3000, arena=4 << 20, max_len=20 << 10):
+    ents = []
+    for i in range(count):
+        n = int(rng.integers(1, max_len))
+        addr = 16 * int(rng.integers(0, (arena - n) // 16))
+        ents.append((1000 + i, addr, rng.integers(0, 256, n, dtype=np.uint8), n + int(rng.integers(0, 64)),
+                     int(rng.random() < 0.1)))
+    return ents
+
+
+def _drain_model(oracle, ents, parity, done, stable, k, lid, self_lid):
+    c = oracle.big_vandermonde(k + 2, k)[self_lid * k + lid]
+    want = parity.copy()
+    applied = vetoed = 0
+    for xid, addr, val, _, veto in ents:  # already in xid order
+        if not done < xid <= stable:
+            continue
+        if veto:
+            vetoed += 1
+            continue
+        oracle.region_multiply(val.copy(), c, want[addr:addr + len(val)], 1)
+        applied += 1
+    return want, applied, vetoed
+
+
+@pytest.mark.gpu
+def test_drain_gf_into_registered_host_arena(gpu, oracle, tmp_path):
+    """The placement the unchanged server runs (ecmem in host memory, read by recovery.c:81
+    and sent by memcached.c:4282 from the host): the arena registered once with
+    cec_host_register and drained by cocytus_drain_gf through its device alias -- the same
+    bytes as the sequential loop, in the host arena itself when the call returns."""
+    _need_exe()
+    k, m, lid, self_lid = 3, 2, 2, 3
+    arena = 4 << 20
+    rng = np.random.default_rng(12)
+    ents = _drain_case(rng, 1500)
+    parity = rng.integers(0, 256, arena, dtype=np.uint8)
+    done, stable = 1000 + 100, 1000 + 1400
+    r, out = run("apply_host", tmp_path, lid=lid, self_lid=self_lid, k=k, m=m, ring=2048, tail=100, entries=ents,
+                 done=done, stable=stable, cap=2048, arena=arena, parity=parity)
+    want, applied, vetoed = _drain_model(oracle, ents, parity, done, stable, k, lid, self_lid)
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), want)
+    assert r.stdout.split()[:4] == ["applied", str(applied), "vetoed", str(vetoed)], r.stdout
+
+
+@pytest.mark.gpu
+def test_drain_refused_window_runs_no_fold(gpu, oracle, tmp_path):
+    """the recovery fold has side effects, so a window the apply would refuse
+    (here a diff larger than the drainer's staging) is refused before ANY fold runs
+    (cec_drainer_validate first): rc CEC_EINVAL, zero hook calls, the arena untouched."""
+    _need_exe()
+    rng = np.random.default_rng(4)
+    ents = [(1 + i, 16 * i * 512, rng.integers(0, 256, n, dtype=np.uint8), n, 0)
+            for i, n in enumerate([100, 4000, 5000, 300])]          # xid 3: 5000 B > 4096
+    parity = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    r, out = run("apply4k", tmp_path, lid=0, self_lid=3, k=3, m=2, ring=8, tail=0, entries=ents, done=0, stable=4,
+                 cap=8, arena=1 << 20, parity=parity)
+    assert r.stdout.split() == ["rc", "-1", "hooks", "0"], r.stdout
+    assert np.array_equal(np.fromfile(out, dtype=np.uint8), parity)
+
+
 @pytest.mark.gpu
 def test_drain_gf_matches_sequential_loop(gpu, oracle, tmp_path):
     """cocytus_drain_gf over 3,000 queued diffs of one data peer (random lengths 1 B -
@@ -144,8 +205,10 @@ def test_collect_under_asan_ubsan(tmp_path):
     subprocess.run(["gcc", "-O1", "-g", "-std=gnu11", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
                     "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration"),
                     "-I", os.path.dirname(ref), "-o", str(exe), os.path.join(ROOT, "tests", "glue", "drain_main.c"),
-                    os.path.join(ROOT, "integration", "cocytus_drain.c"), "-L", os.path.join(ROOT, "cocytus_amd"),
-                    "-lcocytus_ec", "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd")], check=True)
+                    os.path.join(ROOT, "integration", "cocytus_drain.c"), "-I", os.path.join(ROOT, "oracle"),
+                    "-L", os.path.join(ROOT, "cocytus_amd"), "-lcocytus_ec", "-L", os.path.join(ROOT, "oracle"),
+                    "-lgf8ref", "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd"),
+                    "-Wl,-rpath," + os.path.join(ROOT, "oracle")], check=True)
     global EXE
     saved, EXE = EXE, str(exe)
     os.environ["ASAN_OPTIONS"] = "detect_leaks=0"

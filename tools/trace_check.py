@@ -27,7 +27,8 @@ def main(prof_dir, line_path, out_path=None):
     stats = glob.glob(os.path.join(prof_dir, "**", "run_kernel_stats.csv"), recursive=True)
     assert traces, f"no run_kernel_trace.csv under {prof_dir}"
     rows = list(csv.DictReader(open(traces[0])))
-    steps, warm = line["steps"], line["warmup"]
+    # the warmups the bench actually ran (it runs at least one even under --warmup 0)
+    steps, warm = line["steps"], line.get("warmup_run", max(1, line["warmup"]))
     k, m = line["config"]["k"], line["config"]["m"]
     eng = "PermEngine" if "PermEngine" in line["roofline"]["kernel"] else "LdsEngine"
     tiles = line["config"]["stripes_per_gpu"] * line["config"]["value_bytes"] // 4096
