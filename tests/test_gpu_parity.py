@@ -263,8 +263,10 @@ def test_diff_update_full_size(gpu, oracle, engine_name):
     """The north star's per-SET diff-update at the bench's size (65,536 SETs of
     4 KiB, source shard j uniform in {0,1,2}, RS(3,2), install), three rounds of new
     values: the parity arenas stay the encode of the installed data (a size-independent
-    property), checked against the oracle's encode of the whole 256 MiB arenas; and the
-    installed data equal the last round's values."""
+    property), checked against the oracle's encode of the whole 256 MiB arenas; and, per
+    round, every shard equals its value before the round outside the SETs of that shard and
+    the round's staged values inside them (a kernel that installed a SET's value into
+    another shard's range, or left a shard's own range stale, fails)."""
     torch, ec = gpu
     k, m, n, B = 3, 2, 4096, 65536
     T = n * B
@@ -276,20 +278,23 @@ def test_diff_update_full_size(gpu, oracle, engine_name):
     src = np.random.default_rng(6).integers(0, k, B)
     default = ec.get_engine()
     ec.set_engine({"auto": ec.CEC_ENGINE_AUTO, "perm": ec.CEC_ENGINE_PERM, "lds": ec.CEC_ENGINE_LDS}[engine_name])
+    sel = [torch.from_numpy(np.repeat(src == j, n)).cuda() for j in range(k)]  # shard j's SET bytes
     try:
         with ec.Plan([(s * n, s * n, n, int(src[s])) for s in range(B)]) as plan:
-            for _ in range(3):
+            for rnd in range(3):
                 stage = torch.randint(0, 256, (T,), dtype=torch.uint8, device="cuda", generator=g)
+                before = [d.clone() for d in data]
                 ec.diff_update(k, m, mat, data, stage, parity, True, plan)
                 ran = ec.last_engine()
-            torch.cuda.synchronize()
+                torch.cuda.synchronize()
+                for j in range(k):  # each SET installed its value into its own shard only
+                    assert torch.equal(data[j][sel[j]], stage[sel[j]]), f"round {rnd}: install into shard {j}"
+                    assert torch.equal(data[j][~sel[j]], before[j][~sel[j]]), f"round {rnd}: shard {j} off its SETs"
+                del before
     finally:
         ec.set_engine(default)
     if engine_name == "auto":
         assert ran == ec.CEC_ENGINE_PERM
-    for j in range(k):  # each SET installed the last round's value into its own shard only
-        sel = torch.from_numpy(np.repeat(src == j, n)).cuda()
-        assert torch.equal(torch.where(sel, stage, data[j]), data[j]), f"install {j}"
     _assert_parity_matches_oracle(torch, oracle, mat, k, m, data, parity)
 
 
