@@ -4,6 +4,11 @@
  * (compiled against the reference's recovery.h / ecmem.h where they lie).
  *
  *   recovery_bench [REPS]      one JSON line per shape:
+ *   recovery_bench set N SIZE [REPS]
+ *               the data side (integration/cocytus_set.c): the diffs of N SETs of SIZE bytes
+ *               (complete_nread, memcached.c:2664-2681) at shuffled 16-B aligned addresses of a
+ *               host ecmem, values in their own malloc'd buffers: one cocytus_set_diffs_gf
+ *               against the per-SET drop-in call and the restated CPU call (1 thread).
  *
  *   range_1MiB  one recovery request over 256 units (1 MiB), RS(3,2), this parity P1 the
  *               leader of a single loss (D1 lost; mask P1 + D0 + D2, start_recovery's):
@@ -31,6 +36,7 @@
 #include <cocytus_ec.h>
 
 #include "cocytus_recovery.h"
+#include "cocytus_set.h"
 #include "gf8_ref.h" /* oracle: the restated CPU region multiply (baseline only) */
 
 #define K 3
@@ -188,7 +194,81 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
     return same ? 0 : 4;
 }
 
+static int set_bench(int n, int size, int reps) {
+    const size_t stride = ((size_t)size + 15) / 16 * 16, arena = (size_t)n * stride;
+    struct ecmem ecm;
+    memset(&ecm, 0, sizeof ecm);
+    ecm.size = arena;
+    ecm.mem = malloc(arena);
+    fill(ecm.mem, arena, 5);
+    cocytus_set_diff *sd = calloc((size_t)n, sizeof *sd);
+    int *perm = malloc(sizeof(int) * (size_t)n);
+    for (int e = 0; e < n; ++e) perm[e] = e;
+    uint64_t s = 0x9E3779B97F4A7C15ull;
+    for (int e = n - 1; e > 0; --e) {
+        s ^= s << 13, s ^= s >> 7, s ^= s << 17;
+        const int r = (int)(s % (uint64_t)(e + 1)), t = perm[e];
+        perm[e] = perm[r];
+        perm[r] = t;
+    }
+    char *diffs[3];
+    for (int p = 0; p < 3; ++p) diffs[p] = malloc((size_t)n * stride);
+    for (int e = 0; e < n; ++e) {
+        char *v = malloc((size_t)size);
+        fill(v, (size_t)size, 1000 + (uint64_t)e);
+        sd[e].value = v;
+        sd[e].addr = (uint64_t)perm[e] * stride;
+        sd[e].nbytes = (uint32_t)size;
+    }
+    double t[3][64];
+    for (int path = 0; path < 3; ++path) {
+        for (int e = 0; e < n; ++e) sd[e].diff = diffs[path] + (size_t)e * stride;
+        for (int rep = 0; rep <= reps; ++rep) {
+            const double t0 = now_s();
+            if (path == 0) {
+                if (cocytus_set_diffs_gf(&ecm, sd, n, NULL)) return fprintf(stderr, "%s\n", cec_last_error()), 2;
+            } else {
+                for (int e = 0; e < n; ++e) { /* memcached.c:2676-2681 */
+                    memcpy(sd[e].diff, sd[e].value, (size_t)size);
+                    char *old = ecmem_get(&ecm, sd[e].addr);
+                    if (path == 1) galois_w08_region_multiply(old, 1, size, sd[e].diff, 1);
+                    else ref_region_multiply_simd((const uint8_t *)old, 1, size, (uint8_t *)sd[e].diff);
+                }
+            }
+            if (rep) t[path][rep - 1] = now_s() - t0;
+            if (path == 1 && rep == 1) { /* the drop-in loop is slow: one timed pass */
+                t[path][1] = t[path][0];
+                break;
+            }
+        }
+        qsort(t[path], (size_t)(path == 1 ? 2 : reps), sizeof(double), cmp_d);
+    }
+    int same = 1;
+    for (int e = 0; e < n; ++e)
+        same &= !memcmp(diffs[0] + (size_t)e * stride, diffs[1] + (size_t)e * stride, (size_t)size) &&
+                !memcmp(diffs[0] + (size_t)e * stride, diffs[2] + (size_t)e * stride, (size_t)size);
+    const double gib = (double)n * size / (double)(1u << 30);
+    const double med[3] = {t[0][reps / 2], t[1][0], t[2][reps / 2]};
+    cec_batch_stats st;
+    cec_region_multiply_batch_stats(&st);
+    printf("{\"shape\": \"set_diffs\", \"sets\": %d, \"value_bytes\": %d, \"glue_ms\": %.3f, \"glue_GiBps\": %.2f, "
+           "\"dropin_loop_ms\": %.1f, \"dropin_loop_GiBps\": %.3f, \"dropin_us_per_set\": %.2f, "
+           "\"cpu_restated_1thread_ms\": %.3f, \"cpu_restated_1thread_GiBps\": %.2f, \"glue_vs_dropin\": %.1f, "
+           "\"glue_vs_cpu_1thread\": %.2f, \"last_batch\": {\"launches\": %d, \"rounds\": %d, \"pack_us\": %.0f, "
+           "\"gpu_wait_us\": %.0f, \"unpack_us\": %.0f}, \"verified\": %s}\n",
+           n, size, 1e3 * med[0], gib / med[0], 1e3 * med[1], gib / med[1], 1e6 * med[1] / n, 1e3 * med[2],
+           gib / med[2], med[1] / med[0], med[2] / med[0], st.launches, st.rounds, st.pack_us, st.gpu_us,
+           st.unpack_us, same ? "true" : "false");
+    return same ? 0 : 4;
+}
+
 int main(int argc, char **argv) {
+    if (argc >= 4 && !strcmp(argv[1], "set")) {
+        if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
+        const int reps = argc > 4 ? atoi(argv[4]) : 7;
+        if (reps < 1 || reps > 64) return 1;
+        return set_bench(atoi(argv[2]), atoi(argv[3]), reps);
+    }
     const int reps = argc > 1 ? atoi(argv[1]) : 15;
     if (reps < 1 || reps > 64) return 1;
     if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;

@@ -22,6 +22,9 @@
  *   Q ...                       cocytus_recovery_solve_defer (outputs appended at the next F)
  *   F                           cocytus_recovery_flush
  *   P                           list the queued jobs (no GPU needed)
+ *   V N                         cocytus_set_diffs_gf (integration/cocytus_set.c) for the next
+ *                               N lines "ADDR SIZE OFF" (value = HEAP+OFF, old bytes = the arena
+ *                               at ADDR); the diffs appended to OUT.solves
  *   Z LID N DEFER               a drain window during recovery: N queued diffs of data peer
  *                               LID on the next N lines "ADDR SIZE OFF" (xids 1..N), drained by
  *                               cocytus_drain_gf with the recovery fold hook (DEFER: queued
@@ -40,6 +43,7 @@
 
 #include "cocytus_drain.h"
 #include "cocytus_recovery.h"
+#include "cocytus_set.h"
 #include "rep_queue.h"
 
 #define MAXL 64
@@ -262,6 +266,27 @@ int main(int argc, char **argv) {
             free(scratch);
             free(nb);
             free(q.items);
+        } else if (!strcmp(op, "V")) {
+            int n;
+            if (fscanf(sc, "%d", &n) != 1) return 2;
+            cocytus_set_diff *sd = calloc((size_t)n + 1, sizeof *sd);
+            for (int i = 0; i < n; ++i) {
+                unsigned long long addr;
+                unsigned size;
+                long long off;
+                if (fscanf(sc, "%llu %u %lld", &addr, &size, &off) != 3) return 2;
+                sd[i].addr = addr;
+                sd[i].nbytes = size;
+                sd[i].value = heap + off;
+                sd[i].diff = malloc((size_t)size + 16);
+            }
+            const int rc = cocytus_set_diffs_gf(&ecm, sd, n, NULL);
+            fprintf(log, "V %d\n", rc);
+            for (int i = 0; i < n; ++i) {
+                if (rc == 0) fwrite(sd[i].diff, 1, sd[i].nbytes, solves);
+                free(sd[i].diff);
+            }
+            free(sd);
         } else if (!strcmp(op, "P")) {
             const cec_region_job *f, *s;
             int nf, ns;

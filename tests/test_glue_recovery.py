@@ -322,7 +322,8 @@ def test_glue_recovery_under_asan_ubsan(oracle, tmp_path):
                     "-I", os.path.join(ROOT, "include"), "-I", os.path.join(ROOT, "integration"),
                     "-I", os.path.dirname(ref), "-o", str(exe), os.path.join(ROOT, "tests", "glue", "recovery_main.c"),
                     os.path.join(ROOT, "integration", "cocytus_recovery.c"),
-                    os.path.join(ROOT, "integration", "cocytus_drain.c"), "-L", os.path.join(ROOT, "cocytus_amd"),
+                    os.path.join(ROOT, "integration", "cocytus_drain.c"),
+                    os.path.join(ROOT, "integration", "cocytus_set.c"), "-L", os.path.join(ROOT, "cocytus_amd"),
                     "-lcocytus_ec", "-Wl,-rpath," + os.path.join(ROOT, "cocytus_amd")], check=True)
     global EXE
     saved, EXE = EXE, str(exe)
@@ -454,3 +455,33 @@ def test_drain_during_recovery_folds_then_applies(gpu, oracle, tmp_path, defer):
     assert all(v > 0 for v in z), log
     check_state(mod, flags, data, touch)
     assert np.array_equal(arena, mod.heap[:n * U])
+
+
+@pytest.mark.gpu
+def test_set_diffs_batch(gpu, oracle, tmp_path):
+    """The data side (integration/cocytus_set.c): complete_nread's diff of every SET of a
+    pass (memcached.c:2664-2681: diff = new value, then ^= 1 * the old bytes at the value's
+    new arena address), in one batch -- the diffs equal the reference's per-SET chain
+    (values of 1 B - 20 KiB, CRLF-ragged lengths, 16-B aligned addresses as ecalloc.c:176
+    gives, some reusing the same old bytes)."""
+    _need_exe()
+    k, m, s, n = 3, 2, 3, 2048
+    rng, heap, mod, sc = _setup(oracle, k, m, s, n, seed=77)
+    base = n * U
+    sets = []
+    for _ in range(600):
+        size = int(rng.integers(1, 20 << 10)) + 2
+        addr = 16 * int(rng.integers(0, (n * U - size) // 16))
+        off = base + int(rng.integers(0, (8 << 20) - size))
+        sets.append((addr, size, off))
+    sc.add("V", len(sets))
+    for addr, size, off in sets:
+        sc.add(addr, size, off)
+    log, _, _, _, _, diffs = run_script(tmp_path, sc, heap, n, k, m)
+    assert "V 0" in log
+    want = []
+    for addr, size, off in sets:
+        d = heap[off:off + size].copy()                                   # memcpy(diff, c->vbuf)
+        oracle.region_multiply(heap[addr:addr + size].copy(), 1, d, 1)    # ^= 1 * ecmem[addr]
+        want.append(d)
+    assert np.array_equal(diffs, np.concatenate(want))
