@@ -24,7 +24,8 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-EXE = os.path.join(ROOT, "oracle", "_ref", "glue_recovery")
+# (tools/asan.sh runs these tests through a sanitizer build of the same driver)
+EXE = os.environ.get("CEC_GLUE_RECOVERY_EXE") or os.path.join(ROOT, "oracle", "_ref", "glue_recovery")
 U = 4096
 F_UPDATE, F_RECOVERED = 1 << 30, 1 << 31
 

@@ -46,6 +46,26 @@ run)
   timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
       -k "dropin or batched_bindings or concurrent_threads" -p no:cacheprovider
   timeout -k 10 200 "$A/pool_bench.bin"
+  # round 5: the server glue (integration/) and the host-memory batch under it, compiled
+  # against the reference's headers on the CPU (glue build, below) and linked here to the
+  # instrumented library: the GPU glue tests through that binary, then its bench shapes
+  if [ -x "$A/glue_recovery" ]; then
+    CEC_GLUE_RECOVERY_EXE="$A/glue_recovery" timeout -k 10 300 python -u -m pytest tests/test_glue_recovery.py \
+        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
+    timeout -k 10 200 "$A/glue_recovery_bench" 3
+    timeout -k 10 200 "$A/glue_recovery_bench" set 16384 4098 2
+  fi
   ;;
-*) echo "usage: $0 build|run" >&2; exit 2 ;;
+glue)  # (here, on the CPU, where the reference's headers are) the glue programs against tools/asan
+  REF=${REF:-/root/reference}
+  G="-O1 -g -std=gnu11 -fsanitize=address,undefined -fno-sanitize-recover=undefined -shared-libsan -fno-omit-frame-pointer"
+  CC=$ROCM/llvm/bin/clang
+  $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -o "$A/glue_recovery" "$R/tests/glue/recovery_main.c" \
+      "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" "$R/integration/cocytus_set.c" \
+      -L"$A" -lcocytus_ec -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT
+  $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_recovery_bench" \
+      "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_set.c" \
+      -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
+  ;;
+*) echo "usage: $0 build|glue|run" >&2; exit 2 ;;
 esac

@@ -26,6 +26,19 @@ run)
   cd "$R"
   timeout -k 10 300 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread \
       -k "dropin_c_program or reentrant_threads or batched_bindings or concurrent_threads" -p no:cacheprovider
+  # round 5: the host-memory batch's pack pool and pipelined rounds, through the glue bench
+  if [ -x "$T/glue_recovery_bench" ]; then
+    timeout -k 10 300 "$T/glue_recovery_bench" set 16384 4098 2
+    timeout -k 10 300 "$T/glue_recovery_bench" 2
+  fi
   ;;
-*) echo "usage: $0 build|run" >&2; exit 2 ;;
+glue)  # (here, on the CPU) the glue bench against tools/tsan
+  REF=${REF:-/root/reference}
+  RT=$ROCM/lib/llvm/lib/clang/22/lib/linux
+  $ROCM/llvm/bin/clang -O1 -g -std=gnu11 -fsanitize=thread -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" \
+      -o "$T/glue_recovery_bench" "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" \
+      "$R/integration/cocytus_set.c" -L"$T" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
+      -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,--whole-archive $RT/libclang_rt.tsan_cxx-x86_64.a -Wl,--no-whole-archive -lstdc++
+  ;;
+*) echo "usage: $0 build|glue|run" >&2; exit 2 ;;
 esac
