@@ -332,6 +332,24 @@ def test_roofline_traffic_tied_to_the_build(tmp_path, monkeypatch):
     assert bench.load_traffic("rs32_4k", code_id="00112233aabbccdd") == ((None, None), True)
 
 
+def test_host_batch_wave_planning(tmp_path):
+    """cec_region_multiply_batch's planning (cec_hostbatch.inc: the pieces, the range-assign
+    / range-max tree and hb_cluster_waves), spliced from the shipped source into
+    tests/drain_c/hb_waves_main.cpp and run under ASan + UBSan on 4,000 random clusters:
+    overlapping pieces never share a wave, a cluster holding a write keeps job order, an
+    XOR-only cluster takes exactly its overlap depth in waves."""
+    src = open(os.path.join(ROOT, "cocytus_amd", "csrc", "cec_hostbatch.inc")).read()
+    a, b = src.index("enum HbKind"), src.index("struct HbCopy {")
+    prog = open(os.path.join(ROOT, "tests", "drain_c", "hb_waves_main.cpp")).read()
+    cpp = tmp_path / "hb_waves.cpp"
+    cpp.write_text(prog.replace("// HB_FUNCS", src[a:b]))
+    exe = tmp_path / "hb_waves"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-fsanitize=address,undefined", "-fno-sanitize-recover=all",
+                    "-o", str(exe), str(cpp)], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stdout + r.stderr[-2000:]
+
+
 def test_drain_wave_colouring(tmp_path):
     """The drainer's host-side colouring (cec_drain.inc: the radix address sort and the
     greedy interval colouring with its no-overlap fast path), spliced from the shipped

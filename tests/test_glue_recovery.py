@@ -342,23 +342,33 @@ def test_glue_recovery_under_asan_ubsan(oracle, tmp_path):
 
 
 # ----------------------------------------------------------------- GPU: the bytes
+def _solve_masks(rng, k, m, s):
+    """Every loss count 1..m with this parity in the mask (start_recovery's masks: this
+    leader + the other parities it needs + the surviving data lids), and masks without
+    this parity (start_fast_recovery's) where enough other parities exist."""
+    masks = []
+    others = [p for p in range(k, k + m) if p != s]
+    for n_lost in range(1, m + 1):
+        lost = set(int(x) for x in rng.choice(k, n_lost, replace=False))
+        pars = [s] + [int(x) for x in rng.choice(others, n_lost - 1, replace=False)]
+        masks.append(sum(1 << p for p in pars) | sum(1 << j for j in range(k) if j not in lost))
+    for n_lost in range(1, len(others) + 1):
+        lost = set(int(x) for x in rng.choice(k, n_lost, replace=False))
+        pars = [int(x) for x in rng.choice(others, n_lost, replace=False)]
+        masks.append(sum(1 << p for p in pars) | sum(1 << j for j in range(k) if j not in lost))
+    return masks
+
+
 def _solve_ops(rng, mod, sc, n, k, m, s, deferred):
-    """Leader solves over ranges the model says are complete (every data lid of the mask
-    applied): single loss with self in the mask, double loss (self + the other parity's
-    residual from data_from_parity) and a mask without self (start_fast_recovery's)."""
+    """Leader solves over ranges made complete first (every data lid of the mask applied)
+    for every mask of _solve_masks, on unit ranges of 1-4 units: C from this parity's units
+    and the other parities' residuals (data_from_parity), as memcached.c:7868-7922."""
     base = n * U
     want = []
-    for ub, ue, mask in ((0, 3, None), (8, 8, None), (16, 19, "double"), (24, 25, "noself")):
-        if mask is None:
-            lost = int(rng.integers(0, k))
-            mk = (1 << s) | sum(1 << j for j in range(k) if j != lost)
-        elif mask == "double":
-            keep = int(rng.integers(0, k))
-            mk = (1 << k) | (1 << (k + 1)) | (1 << keep)
-        else:
-            lost = int(rng.integers(0, k))
-            other = k + (1 - (s - k))
-            mk = (1 << other) | sum(1 << j for j in range(k) if j != lost)
+    for q, mk in enumerate(_solve_masks(rng, k, m, s)):
+        ub = 4 * q
+        ue = ub + int(rng.integers(0, 4))
+        assert ue < n
         dfp = [-1] * (k + m)
         for p in range(k, k + m):
             if mk >> p & 1 and p != s:
@@ -367,14 +377,12 @@ def _solve_ops(rng, mod, sc, n, k, m, s, deferred):
             for j in range(k):
                 if mk >> j & 1:
                     todo = [i for i in range(ub, ue + 1) if not mod.flags[i] & (1 << j)]
+                    if any(mod.flags[i] & F_RECOVERED for i in todo):
+                        continue
                     for i in todo:
-                        if mod.flags[i] & F_RECOVERED:
-                            break
-                    else:
-                        for i in todo:
-                            off = base + int(rng.integers(0, (8 << 20) - U))
-                            sc.add("D" if deferred else "R", j, i, i, off)
-                            mod.recover(j, i, i, off, defer=False)
+                        off = base + int(rng.integers(0, (8 << 20) - U))
+                        sc.add("D" if deferred else "R", j, i, i, off)
+                        mod.recover(j, i, i, off, defer=False)
         sc.add("Q" if deferred else "S", ub, ue, mk, *dfp)
         rc, out = mod.solve(ub, ue, mk, dfp)
         want.append((rc, out))
@@ -382,13 +390,15 @@ def _solve_ops(rng, mod, sc, n, k, m, s, deferred):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(8))
 def test_glue_bytes_match_reference_chain(gpu, oracle, tmp_path, seed):
     """Immediate and deferred forms mixed (R/T/W and D/t/w, a flush at the end), then
-    leader solves: every unit byte, flag, touch flag and solve output equals the
-    reference's per-unit chain run by the model."""
+    leader solves for every loss count up to m: every unit byte, flag, touch flag and solve
+    output equals the reference's per-unit chain run by the model.  RS(3,2) (seeds 0-3),
+    RS(4,2) (4-5) and RS(6,3) (6-7), this parity rotating over the parity lids."""
     _need_exe()
-    k, m, s, n = 3, 2, 3 + seed % 2, 48
+    k, m = ([(3, 2)] * 4 + [(4, 2)] * 2 + [(6, 3)] * 2)[seed]
+    s, n = k + seed % m, 48
     heap, mod, sc = _random_script(oracle, seed, k, m, s, n, gpu_ops=True)
     sc.add("F")
     _apply_model_queue(mod)
