@@ -254,10 +254,10 @@ static int set_bench(int n, int size, int reps) {
     printf("{\"shape\": \"set_diffs\", \"sets\": %d, \"value_bytes\": %d, \"glue_ms\": %.3f, \"glue_GiBps\": %.2f, "
            "\"dropin_loop_ms\": %.1f, \"dropin_loop_GiBps\": %.3f, \"dropin_us_per_set\": %.2f, "
            "\"cpu_restated_1thread_ms\": %.3f, \"cpu_restated_1thread_GiBps\": %.2f, \"glue_vs_dropin\": %.1f, "
-           "\"glue_vs_cpu_1thread\": %.2f, \"last_batch\": {\"launches\": %d, \"rounds\": %d, \"pack_us\": %.0f, "
-           "\"gpu_wait_us\": %.0f, \"unpack_us\": %.0f}, \"verified\": %s}\n",
+           "\"glue_vs_cpu_1thread\": %.2f, \"last_batch\": {\"launches\": %d, \"rounds\": %d, \"plan_us\": %.0f, "
+           "\"pack_us\": %.0f, \"gpu_wait_us\": %.0f, \"unpack_us\": %.0f}, \"verified\": %s}\n",
            n, size, 1e3 * med[0], gib / med[0], 1e3 * med[1], gib / med[1], 1e6 * med[1] / n, 1e3 * med[2],
-           gib / med[2], med[1] / med[0], med[2] / med[0], st.launches, st.rounds, st.pack_us, st.gpu_us,
+           gib / med[2], med[1] / med[0], med[2] / med[0], st.launches, st.rounds, st.plan_us, st.pack_us, st.gpu_us,
            st.unpack_us, same ? "true" : "false");
     return same ? 0 : 4;
 }

@@ -63,7 +63,7 @@ def test_batch_disjoint_matches_sequential(gpu, oracle, align):
     want = _model(oracle, heap, jobs)
     launches, rounds = _run(ec, heap, jobs)
     assert np.array_equal(heap, want)
-    assert launches == 1 and rounds == 1
+    assert launches == rounds  # disjoint destinations: one wave per staging round (pipelined rounds above 4 MiB)
 
 
 def test_batch_recovery_units_shape(gpu, oracle):
