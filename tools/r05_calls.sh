@@ -20,5 +20,26 @@ e)  # host code under ASan + UBSan and TSan, incl. the round-5 glue and host bat
     timeout -k 10 900 bash tools/asan.sh run > $out/asan.txt 2>&1 || exit 1
     timeout -k 10 900 bash tools/tsan.sh run > $out/tsan.txt 2>&1 || exit 2
     ;;
+f)  # the final tree as the driver runs it: smoke, the whole GPU suite (incl. the one-rank
+    # RCCL path and configs[3]'s eight rank batches on one card), the default line
+    out=gpurun_out/r05f; mkdir -p $out
+    timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit 1
+    timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $out/pytest.log 2>&1
+    rc=$?; echo "pytest rc=$rc"; [ $rc -gt 1 ] && exit $rc
+    timeout -k 10 300 python -u bench.py > $out/bench_default.jsonl 2> $out/bench_default.err || exit 3
+    ;;
+g)  # rocprofv3 --kernel-trace --stats of the driver's exact command (python bench.py, no
+    # flags) with its line, for tools/trace_check.py
+    out=$GRAFT_REPO_ROOT/gpurun_out/r05g; mkdir -p $out
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_r05_default" -o run \
+        --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" > $out/bench_default.jsonl 2> $out/bench_default.err
+    ;;
+h)  # where the host batch's GPU time goes: kernel durations of the recovery shapes
+    out=$GRAFT_REPO_ROOT/gpurun_out/r05h; mkdir -p $out
+    cd /tmp && export TMPDIR=/tmp
+    timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/prof" -o run --output-format csv \
+        -- python3 "$GRAFT_REPO_ROOT/tools/hostbatch_bench.py" 5 > $out/hostbatch_bench.jsonl 2> $out/err.log
+    ;;
 *) echo "unknown case $1"; exit 9 ;;
 esac
