@@ -259,6 +259,11 @@ static int set_bench(int n, int size, int reps) {
            n, size, 1e3 * med[0], gib / med[0], 1e3 * med[1], gib / med[1], 1e6 * med[1] / n, 1e3 * med[2],
            gib / med[2], med[1] / med[0], med[2] / med[0], st.launches, st.rounds, st.plan_us, st.pack_us, st.gpu_us,
            st.unpack_us, same ? "true" : "false");
+    for (int e = 0; e < n; ++e) free((void *)sd[e].value);
+    for (int p = 0; p < 3; ++p) free(diffs[p]);
+    free(sd);
+    free(perm);
+    free(ecm.mem);
     return same ? 0 : 4;
 }
 
