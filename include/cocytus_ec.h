@@ -266,7 +266,10 @@ uint8_t *cec_drainer_staging(cec_drainer *d, size_t *capacity);
  * commutes).  A src or base range must not overlap any job's dst (CEC_EOVERLAP; base ==
  * dst is the in-place add).  Every pointer is HOST memory (pageable, pinned or registered;
  * device-resident state uses the device ops above).  Synchronous: on return every dst
- * holds its bytes.  Lengths and alignments are arbitrary. */
+ * holds its bytes.  Lengths and alignments are arbitrary.  Staging is per calling thread:
+ * mapped pinned memory, up to 2 x 24 MiB (more for one larger overlapping cluster), kept
+ * for the thread's next call; batches above 4 MiB are pipelined over double-buffered
+ * rounds.  A HIP failure (CEC_EHIP) may leave some destinations written and others not. */
 typedef struct cec_region_job {
     const void *src;    /* region (read) */
     void *dst;          /* r2 (written) */

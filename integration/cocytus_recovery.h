@@ -120,7 +120,10 @@ int cocytus_recovery_solve_defer(cocytus_rglue *g, struct recovery *r, const str
                                  char **data, int *n_out);
 
 /* Run every queued fold (one batch), then every queued solve (one batch).  Returns the
- * number of queued requests run (folds + solves) or a negative cec_status. */
+ * number of queued requests run (folds + solves) or a negative cec_status.  On a failure
+ * the queues are kept but some folds may have landed: the recovery state is undefined and
+ * the process must stop (a retry could fold twice); the data[] buffers of queued solves
+ * stay the caller's to free. */
 int cocytus_recovery_flush(cocytus_rglue *g);
 
 /* Queued requests (folds + solves) not yet flushed. */
