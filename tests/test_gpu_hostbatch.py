@@ -198,3 +198,25 @@ def test_batch_pinned_host_buffers(gpu, oracle):
     want = _model(oracle, heap, jobs)
     _run(ec, heap, jobs)
     assert np.array_equal(heap, want)
+
+
+def test_batch_fuzz_small(gpu, oracle):
+    """300 random small batches (1-60 jobs of 1 B - 12 KiB, every kind, dense or sparse
+    overlap of destinations, unaligned everything, base == dst now and then): each equals
+    the sequential chain."""
+    torch, ec = gpu
+    rng = np.random.default_rng(2024)
+    heap = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
+    for it in range(300):
+        span = int(rng.choice([16 << 10, 256 << 10, 2 << 20]))     # destination region: overlap density
+        jobs = []
+        for _ in range(int(rng.integers(1, 61))):
+            n = int(rng.integers(1, 12 << 10))
+            d = int(rng.integers(0, span - n)) if span > n else 0
+            s = (2 << 20) + int(rng.integers(0, (2 << 20) - n))
+            kind = rng.choice(["xor", "xor", "write", "base", "inplace"])
+            b = (2 << 20) + int(rng.integers(0, (2 << 20) - n)) if kind == "base" else (d if kind == "inplace" else None)
+            jobs.append((s, d, b, n, int(rng.integers(0, 256)), 0 if kind == "write" else 1))
+        want = _model(oracle, heap, jobs)
+        _run(ec, heap, jobs)
+        assert np.array_equal(heap, want), f"iteration {it}"
