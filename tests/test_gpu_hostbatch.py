@@ -220,3 +220,23 @@ def test_batch_fuzz_small(gpu, oracle):
         want = _model(oracle, heap, jobs)
         _run(ec, heap, jobs)
         assert np.array_equal(heap, want), f"iteration {it}"
+
+
+def test_batch_refused_while_capturing(gpu, oracle):
+    """The batch is synchronous (it waits for its own launches and then copies the results
+    out): on a stream being captured into a graph it is refused (CEC_EINVAL) before
+    anything is launched, and the capture is unharmed."""
+    torch, ec = gpu
+    heap = np.arange(1 << 16, dtype=np.uint32).view(np.uint8)[:1 << 18].copy()
+    keep = heap.copy()
+    s = torch.cuda.Stream()
+    x = torch.zeros(16, device="cuda")
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        with pytest.raises(ec.CecError) as e:
+            _run(ec, heap, [(128 << 10, 0, None, 4096, 7, 1)], stream=s)
+        assert e.value.code == ec.CEC_EINVAL
+        x.add_(1)
+    g.replay()
+    torch.cuda.synchronize()
+    assert float(x.sum()) == 16.0 and np.array_equal(heap, keep)
