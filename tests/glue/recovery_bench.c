@@ -10,6 +10,10 @@
  *               host ecmem, values in their own malloc'd buffers: one cocytus_set_diffs_gf
  *               against the per-SET drop-in call and the restated CPU call (1 thread).
  *
+ * Every rep recovers other units (32 MiB further into a host arena of (REPS + 2) x 32 MiB), so
+ * the parity bytes of the first touch come cold from memory in every path, as they do when a
+ * recovery walks the arena; the replies are hot (just received).
+ *
  *   range_1MiB  one recovery request over 256 units (1 MiB), RS(3,2), this parity P1 the
  *               leader of a single loss (D1 lost; mask P1 + D0 + D2, start_recovery's):
  *               two data peers' replies (recovery_recover_units, recovery.c:61-96), then
@@ -80,8 +84,11 @@ static char *ref_solve(struct recovery *r, int ub, int ue, int inv, mul_fn mul) 
     return out;
 }
 
+enum { kRepStride = 8192 }; /* units (32 MiB) between the ranges of consecutive reps */
+
 static void reset(struct recovery *r, int nunits) {
     for (int i = 0; i < nunits; ++i) {
+        if (!r->units[i].data && !r->units[i].flags) continue;
         free(r->units[i].data);
         r->units[i].data = NULL;
         r->units[i].flags = 0;
@@ -125,15 +132,17 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
     for (int p = 0; p < 3; ++p) out[p] = calloc((size_t)nreq, sizeof(char *));
     double t[3][64];
     struct recovery_queue_item *it = calloc((size_t)nreq, sizeof *it);
-    for (int q = 0; q < nreq; ++q) {
-        it[q].unit_begin = starts[q];
-        it[q].unit_end = starts[q] + units - 1;
-        it[q].mask = mask;
-    }
+    for (int q = 0; q < nreq; ++q) it[q].mask = mask;
     for (int path = 0; path < 3; ++path) {
         for (int rep = 0; rep <= reps; ++rep) { /* rep 0: warm-up */
             reset(&r, nunits);
             for (int q = 0; q < nreq; ++q) free(out[path][q]);
+            /* each rep recovers other units of the arena (32 MiB further on), so their parity
+             * bytes come cold from host memory, as a recovery scanning the arena reads them */
+            for (int q = 0; q < nreq; ++q) {
+                it[q].unit_begin = starts[q] + rep * kRepStride;
+                it[q].unit_end = it[q].unit_begin + units - 1;
+            }
             const double t0 = now_s();
             if (path == 0) {
                 for (int q = 0; q < nreq; ++q)
@@ -278,7 +287,8 @@ int main(int argc, char **argv) {
     if (reps < 1 || reps > 64) return 1;
     if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
     matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
-    const int nunits = 8192; /* a 32 MiB parity arena, host memory (the server's ecmem) */
+    /* a (reps + 2) x 32 MiB parity arena, host memory (the server's ecmem), walked in 32 MiB steps */
+    const int nunits = 8192 * (reps + 1) + 8192;
     struct ecmem ecm;
     memset(&ecm, 0, sizeof ecm);
     ecm.size = (uint64_t)nunits * U;
@@ -294,7 +304,7 @@ int main(int argc, char **argv) {
         int ok;
         do {
             s ^= s << 13, s ^= s >> 7, s ^= s << 17;
-            starts[q] = 512 + (int)(s % (uint64_t)(nunits - 512));
+            starts[q] = 512 + (int)(s % (uint64_t)(kRepStride - 512)); /* scattered in the rep's 32 MiB */
             ok = 1;
             for (int x = 0; x < q; ++x) ok &= starts[x] != starts[q];
         } while (!ok);
