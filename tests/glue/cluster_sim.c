@@ -4,7 +4,7 @@
  * (rep_queue.h, recovery.h, ecmem.h where they lie), to check the glue end to end against
  * the one truth that needs no oracle: the bytes a lost data shard held.
  *
- *   cluster_sim SEED [DEFER [CONTROL]]
+ *   cluster_sim SEED [DEFER [CONTROL [NLOST_MAX]]]   (NLOST_MAX: at most this many data lids lost, <= M)
  *
  * CONTROL = 1 breaks the protocol on purpose (a reply applied before its peer's queued diffs
  * are drained): the rebuilt bytes must then differ -- the check has teeth.
@@ -43,8 +43,12 @@
 #include "gf8_ref.h" /* oracle: the final parity check only */
 #include "rep_queue.h"
 
+#ifndef K /* the code: -DK= -DM= (default RS(3,2)) */
 #define K 3
+#endif
+#ifndef M
 #define M 2
+#endif
 #define NU 512 /* units per arena: 2 MiB */
 #define U ((size_t)UNITSIZE)
 #define QCAP 4096
@@ -73,7 +77,7 @@ static int *matrix;
 static struct ecmem data[K];
 static struct parity par[M];
 static uint64_t next_xid[K];
-static int sets, folds_possible;
+static int sets;
 
 static uint32_t item_nbytes(void *item, void *ctx) {
     (void)ctx;
@@ -152,9 +156,12 @@ static void set(int j, int defer_unused) {
 
 int main(int argc, char **argv) {
     if (argc < 2) return 1;
-    rng_s = 0x9E3779B97F4A7C15ull ^ (uint64_t)atoll(argv[1]) * 0x2545F4914F6CDD1Dull;
+    const uint64_t seed = (uint64_t)atoll(argv[1]);
+    rng_s = 0x9E3779B97F4A7C15ull ^ seed * 0x2545F4914F6CDD1Dull;
     const int defer = argc > 2 && atoi(argv[2]);
     const int control = argc > 3 && atoi(argv[3]);
+    const int nlost_max = argc > 4 ? atoi(argv[4]) : M;
+    if (nlost_max < 1) return 1;
     if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
     matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
     for (int j = 0; j < K; ++j) {
@@ -190,63 +197,100 @@ int main(int argc, char **argv) {
     }
     for (int p = 0; p < M; ++p)
         for (int j = 0; j < K; ++j) drain(&par[p], j, 0);
-    /* data lid LOST fails: its arena is the truth; the leader parity recovers ranges */
-    const int lost = (int)(rnd() % K);
+    /* NL data lids fail (1 <= NL <= M): their arenas are the truth.  The leader parity
+     * recovers ranges with start_recovery's mask (memcached.c:8136-8151: itself, then the
+     * first K-1 connected lids in lid order -- the surviving data lids, then other
+     * parities); every parity of the mask folds the survivors' replies (recover_units_reply
+     * goes to each, :4277-4282) and the non-leaders ship their units to the leader
+     * (send_recovered_data, :7822-7834, into rqit->data_from_parity) before it solves. */
+    const int nl = 1 + (int)(seed % (uint64_t)(nlost_max < M ? nlost_max : M)); /* every count over the seeds */
+    int lost[M], is_lost[K] = {0};
+    for (int x = 0; x < nl;) {
+        const int j = (int)(rnd() % K);
+        if (!is_lost[j]) is_lost[j] = 1, x++;
+    }
+    for (int j = 0, x = 0; j < K; ++j)
+        if (is_lost[j]) lost[x++] = j;
     struct parity *L = &par[rnd() % M];
-    const uint32_t mask = (1u << L->lid) | (((1u << K) - 1) & ~(1u << lost));
+    uint32_t mask = 1u << L->lid;
+    for (int i = 0, remaining = K - 1; i < K + M && remaining; ++i) {
+        if (i == L->lid || (i < K && is_lost[i])) continue;
+        mask |= 1u << i;
+        remaining--;
+    }
+    struct parity *part[M];
+    int np = 0;
+    for (int p = 0; p < M; ++p)
+        if (mask & (1u << par[p].lid)) part[np++] = &par[p];
     int ranges = 0, bad = 0;
     for (int ub = 0; ub < NU && !bad;) {
         const int span = (int)(rnd() % 24);
         const int ue = ub + span < NU - 1 ? ub + span : NU - 1;
+        const size_t nbuf = (size_t)(ue - ub + 1) * U;
         /* replies arrive in a random order, SETs and drains before, between and after */
         int order[K], no = 0;
         for (int j = 0; j < K; ++j)
-            if (j != lost) order[no++] = j;
-        if (rnd() % 2 && no == 2) {
-            const int t = order[0];
-            order[0] = order[1];
-            order[1] = t;
+            if (!is_lost[j]) order[no++] = j;
+        for (int x = no - 1; x > 0; --x) {
+            const int y = (int)(rnd() % (uint64_t)(x + 1)), t = order[x];
+            order[x] = order[y];
+            order[y] = t;
         }
         for (int r = 0; r <= no; ++r) {
             const int burst = (int)(rnd() % 12);
             for (int i = 0; i < burst; ++i) {
                 int j;
                 do j = (int)(rnd() % K);
-                while (j == lost);
+                while (is_lost[j]);
                 set(j, 0);
-                if (rnd() % 3 == 0) drain(L, j, defer); /* folds into the units during recovery */
+                if (rnd() % 3 == 0) drain(part[rnd() % np], j, defer); /* folds into the units */
             }
             if (r == no) break;
             const int peer = order[r];
-            if (!control) drain(L, peer, defer); /* recover_units_reply: the peer's xids first (:4311-4316) */
-            char *reply = malloc((size_t)(ue - ub + 1) * U);
-            memcpy(reply, (char *)data[peer].mem + (size_t)ub * U, (size_t)(ue - ub + 1) * U);
-            const int rc = defer ? cocytus_recover_units_defer(L->g, &L->rec, &L->ecm, peer, ub, ue, reply, 1)
-                                 : cocytus_recover_units_gf(L->g, &L->rec, &L->ecm, peer, ub, ue, reply);
-            if (!defer) free(reply);
-            if (rc) return fprintf(stderr, "recover: %d %s\n", rc, cec_last_error()), 2;
-            folds_possible++;
+            for (int q = 0; q < np; ++q) { /* each parity of the mask gets the reply */
+                struct parity *P = part[q];
+                if (!control) drain(P, peer, defer); /* recover_units_reply: the peer's xids first (:4311-4316) */
+                char *reply = malloc(nbuf);
+                memcpy(reply, (char *)data[peer].mem + (size_t)ub * U, nbuf);
+                const int rc = defer ? cocytus_recover_units_defer(P->g, &P->rec, &P->ecm, peer, ub, ue, reply, 1)
+                                     : cocytus_recover_units_gf(P->g, &P->rec, &P->ecm, peer, ub, ue, reply);
+                if (!defer) free(reply);
+                if (rc) return fprintf(stderr, "recover: %d %s\n", rc, cec_last_error()), 2;
+            }
         }
         struct recovery_queue_item it;
         memset(&it, 0, sizeof it);
         it.unit_begin = ub;
         it.unit_end = ue;
         it.mask = mask;
+        char *dfp[K + M];
+        memset(dfp, 0, sizeof dfp);
+        it.data_from_parity = dfp;
+        for (int q = 0; q < np; ++q) {
+            struct parity *P = part[q];
+            if (defer && cocytus_recovery_flush(P->g) < 0) return fprintf(stderr, "flush: %s\n", cec_last_error()), 2;
+            if (P == L) continue;
+            dfp[P->lid] = malloc(nbuf); /* send_recovered_data: its units, in order */
+            for (int i = ub; i <= ue; ++i) memcpy(dfp[P->lid] + (size_t)(i - ub) * U, P->rec.units[i].data, U);
+        }
         char *out[M];
         int n = 0;
-        if (defer && cocytus_recovery_flush(L->g) < 0) return fprintf(stderr, "flush: %s\n", cec_last_error()), 2;
-        if (cocytus_recovery_solve_gf(L->g, &L->rec, &it, out, &n) || n != 1)
-            return fprintf(stderr, "solve: %s\n", cec_last_error()), 2;
-        if (memcmp(out[0], (char *)data[lost].mem + (size_t)ub * U, (size_t)(ue - ub + 1) * U)) {
-            printf("range [%d, %d]: rebuilt bytes differ from the lost shard\n", ub, ue);
-            bad = 1;
+        if (cocytus_recovery_solve_gf(L->g, &L->rec, &it, out, &n) || n != nl)
+            return fprintf(stderr, "solve: n %d of %d: %s\n", n, nl, cec_last_error()), 2;
+        for (int x = 0; x < n; ++x) {
+            if (memcmp(out[x], (char *)data[lost[x]].mem + (size_t)ub * U, nbuf) && !bad) {
+                printf("range [%d, %d]: rebuilt bytes of lid %d differ from the lost shard\n", ub, ue, lost[x]);
+                bad = 1;
+            }
+            free(out[x]);
         }
-        free(out[0]);
-        for (int i = ub; i <= ue; ++i) { /* recovery_req_remove (recovery.c:196-205) */
-            free(L->rec.units[i].data);
-            L->rec.units[i].data = NULL;
-            L->rec.units[i].flags = 0;
-        }
+        for (int l = 0; l < K + M; ++l) free(dfp[l]);
+        for (int q = 0; q < np; ++q) /* recovery_req_remove (recovery.c:196-205) */
+            for (int i = ub; i <= ue; ++i) {
+                free(part[q]->rec.units[i].data);
+                part[q]->rec.units[i].data = NULL;
+                part[q]->rec.units[i].flags = 0;
+            }
         ranges++;
         ub = ue + 1;
     }
@@ -262,7 +306,7 @@ int main(int argc, char **argv) {
         }
         free(want);
     }
-    if (!bad) printf("ok ranges %d sets %d lost %d leader %d\n", ranges, sets, lost, L->lid);
+    if (!bad) printf("ok RS(%d,%d) ranges %d sets %d lost %d data lids, leader %d\n", K, M, ranges, sets, nl, L->lid);
     for (int p = 0; p < M; ++p) {
         cocytus_rglue_destroy(par[p].g);
         cec_drainer_destroy(par[p].dr);

@@ -504,18 +504,24 @@ SIM = os.path.join(ROOT, "oracle", "_ref", "glue_cluster_sim")
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("defer", [0, 1])
-def test_cluster_sim_rebuilds_the_lost_shard(gpu, seed, defer):
+@pytest.mark.parametrize("code", ["", "63"])
+def test_cluster_sim_rebuilds_the_lost_shard(gpu, seed, defer, code):
     """An RS(3,2) group in one process through all the glue (tests/glue/cluster_sim.c): SET
     diffs from every data process queued at both parities and drained through the recovery
     fold hook into registered host arenas; a data process lost mid-stream; the leader
     parity rebuilds every unit range while the survivors keep writing (each reply applied
     after that peer's queue is drained, drains folding at random moments, immediate or
-    deferred).  Every rebuilt range equals the bytes the lost shard held -- a truth that
-    needs no oracle -- and the parities end as the code of the data."""
-    if not os.path.exists(SIM):
-        pytest.skip("oracle/_ref/glue_cluster_sim not built (make -C oracle ref)")
-    r = subprocess.run([SIM, str(seed), str(defer)], capture_output=True, text=True, timeout=300)
+    deferred).  RS(3,2) and RS(6,3) (code "63"), 1..M data lids lost: every parity of
+    start_recovery's mask folds the replies and the non-leaders ship their units to the
+    leader (data_from_parity).  Every rebuilt range equals the bytes the lost shards held --
+    a truth that needs no oracle -- and the parities end as the code of the data."""
+    exe = SIM + code
+    if not os.path.exists(exe):
+        pytest.skip(f"{exe} not built (make -C oracle ref)")
+    r = subprocess.run([exe, str(seed), str(defer)], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
+    m = 3 if code == "63" else 2
+    assert f"lost {1 + seed % m} data lids" in r.stdout, r.stdout  # every loss count over the seeds
 
 
 @pytest.mark.gpu
@@ -525,5 +531,5 @@ def test_cluster_sim_control_breaks_without_the_drain(gpu):
     memcached.c:4311-4316) -- must rebuild wrong bytes: the check above detects a wrong fold."""
     if not os.path.exists(SIM):
         pytest.skip("oracle/_ref/glue_cluster_sim not built (make -C oracle ref)")
-    r = subprocess.run([SIM, "0", "0", "1"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([SIM, "0", "0", "1", "1"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "differ" in r.stdout, r.stdout + r.stderr
