@@ -54,6 +54,7 @@ run)
         -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
     timeout -k 10 200 "$A/glue_recovery_bench" 3
     timeout -k 10 200 "$A/glue_recovery_bench" set 16384 4098 2
+    for s in 0 1 2; do timeout -k 10 200 "$A/glue_cluster_sim63" $s $((s % 2)); done
   fi
   ;;
 glue)  # (here, on the CPU, where the reference's headers are) the glue programs against tools/asan
@@ -63,6 +64,10 @@ glue)  # (here, on the CPU, where the reference's headers are) the glue programs
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -o "$A/glue_recovery" "$R/tests/glue/recovery_main.c" \
       "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" "$R/integration/cocytus_set.c" \
       -L"$A" -lcocytus_ec -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT
+  $CC $G -DK=6 -DM=3 -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_cluster_sim63" \
+      "$R/tests/glue/cluster_sim.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" \
+      "$R/integration/cocytus_set.c" -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
+      -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_recovery_bench" \
       "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_set.c" \
       -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
