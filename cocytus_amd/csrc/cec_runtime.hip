@@ -1343,6 +1343,7 @@ CEC_API int cec_host_register(void *p, size_t bytes, uint8_t **device_alias) {
         return fail(CEC_EHIP, "cec_host_register: hipHostGetDevicePointer: %s", hipGetErrorString(e));
     }
     *device_alias = static_cast<uint8_t *>(d);
+    host_region_add(p, bytes, *device_alias, dev);  // (the host batch reads bases there in place)
     return CEC_OK;
 }
 
@@ -1350,6 +1351,7 @@ CEC_API int cec_host_unregister(void *p) {
     if (!p) return fail(CEC_EINVAL, "cec_host_unregister: NULL");
     int dev;
     if (int r = current_device(&dev)) return r;
+    host_region_remove(p);
     HIP_TRY(hipHostUnregister(p));
     return CEC_OK;
 }

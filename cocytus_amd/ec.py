@@ -88,7 +88,8 @@ class RegionJob(ctypes.Structure):
 class BatchStats(ctypes.Structure):
     """cec_batch_stats: the thread's last cec_region_multiply_batch."""
     _fields_ = [("launches", ctypes.c_int), ("rounds", ctypes.c_int), ("plan_us", ctypes.c_float),
-                ("pack_us", ctypes.c_float), ("gpu_us", ctypes.c_float), ("unpack_us", ctypes.c_float)]
+                ("pack_us", ctypes.c_float), ("gpu_us", ctypes.c_float), ("unpack_us", ctypes.c_float),
+                ("in_place_launches", ctypes.c_int)]
 
 
 class CacheInfo(ctypes.Structure):
@@ -791,6 +792,20 @@ def region_multiply_batch(jobs, stream=None) -> tuple[int, int]:
     _check(lib().cec_region_multiply_batch(arr, len(jobs), _stream(stream)))
     st = batch_stats()
     return st["launches"], st["rounds"]
+
+
+def host_register(buf) -> int:
+    """cec_host_register of a host buffer (numpy array / bytearray / address, nbytes from
+    the array): returns its device alias.  Unregister with host_unregister(buf)."""
+    addr = _host_or_dev(buf)
+    n = buf.nbytes if hasattr(buf, "nbytes") else len(buf)
+    alias = ctypes.c_void_p()
+    _check(lib().cec_host_register(addr, n, ctypes.byref(alias)))
+    return alias.value
+
+
+def host_unregister(buf) -> None:
+    _check(lib().cec_host_unregister(_host_or_dev(buf)))
 
 
 def batch_stats() -> dict:

@@ -265,7 +265,9 @@ uint8_t *cec_drainer_staging(cec_drainer *d, size_t *capacity);
  * applied in separate launches (in job order when one of them writes; XOR accumulation
  * commutes).  A src or base range must not overlap any job's dst (CEC_EOVERLAP; base ==
  * dst is the in-place add).  Every pointer is HOST memory (pageable, pinned or registered;
- * device-resident state uses the device ops above).  Synchronous: on return every dst
+ * device-resident state uses the device ops above).  Bases inside a region registered with
+ * cec_host_register (the server's ecmem) are read in place through its device alias when
+ * no two destinations of a staging round overlap: one copy less.  Synchronous: on return every dst
  * holds its bytes.  Lengths and alignments are arbitrary.  Staging is per calling thread:
  * mapped pinned memory, up to 2 x 24 MiB (more for one larger overlapping cluster), kept
  * for the thread's next call; batches above 4 MiB are pipelined over double-buffered
@@ -287,6 +289,7 @@ int cec_region_multiply_batch(const cec_region_job *jobs, int n, void *stream);
 typedef struct cec_batch_stats {
     int launches, rounds;
     float plan_us, pack_us, gpu_us, unpack_us;
+    int in_place_launches; /* launches that read their bases in place (cec_host_register'd) */
 } cec_batch_stats;
 int cec_region_multiply_batch_stats(cec_batch_stats *out);
 

@@ -164,9 +164,13 @@ int main(int argc, char **argv) {
     if (nlost_max < 1) return 1;
     if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
     matrix = reed_sol_big_vandermonde_distribution_matrix(K + M, K, 8);
-    for (int j = 0; j < K; ++j) {
+    for (int j = 0; j < K; ++j) { /* the data processes' ecmem, registered (SET diffs read the
+                                     old bytes in place) */
         data[j].size = NU * U;
-        data[j].mem = calloc(NU, U);
+        if (posix_memalign(&data[j].mem, 4096, NU * U)) return 2;
+        memset(data[j].mem, 0, NU * U);
+        uint8_t *alias;
+        if (cec_host_register(data[j].mem, NU * U, &alias)) return fprintf(stderr, "%s\n", cec_last_error()), 2;
         next_xid[j] = 1;
     }
     for (int p = 0; p < M; ++p) {
@@ -307,6 +311,7 @@ int main(int argc, char **argv) {
         free(want);
     }
     if (!bad) printf("ok RS(%d,%d) ranges %d sets %d lost %d data lids, leader %d\n", K, M, ranges, sets, nl, L->lid);
+    for (int j = 0; j < K; ++j) cec_host_unregister(data[j].mem);
     for (int p = 0; p < M; ++p) {
         cocytus_rglue_destroy(par[p].g);
         cec_drainer_destroy(par[p].dr);

@@ -57,6 +57,7 @@ static void mul_cpu(char *region, int c, int n, char *r2) {
 
 static int *matrix;
 #define MAT(x, y) matrix[(x) * K + (y)]
+static int register_ecmem = 1; /* RECOVERY_BENCH_STAGED=1: leave ecmem unregistered (every base staged) */
 
 /* recovery_recover_units (recovery.c:61-96), per unit */
 static void ref_recover(struct recovery *r, struct ecmem *ecm, int peer, int ub, int ue, char *data, mul_fn mul) {
@@ -186,10 +187,11 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
            "\"payload_MiB\": %.3f, \"glue_us\": %.1f, \"glue_GiBps\": %.3f, \"dropin_loop_us\": %.1f, "
            "\"dropin_loop_GiBps\": %.3f, \"cpu_restated_1thread_us\": %.1f, \"cpu_restated_1thread_GiBps\": %.3f, "
            "\"glue_vs_dropin\": %.1f, \"glue_vs_cpu_1thread\": %.2f, \"reps\": %d, "
-           "\"last_batch\": {\"launches\": %d, \"pack_us\": %.1f, \"gpu_us\": %.1f, \"unpack_us\": %.1f}, "
+           "\"ecmem_registered\": %d, \"last_batch\": {\"launches\": %d, \"in_place\": %d, \"pack_us\": %.1f, \"gpu_us\": %.1f, \"unpack_us\": %.1f}, "
            "\"verified\": %s}\n",
            name, nreq, units, bytes / (1 << 20), 1e6 * med[0], gib / med[0], 1e6 * med[1], gib / med[1], 1e6 * med[2],
-           gib / med[2], med[1] / med[0], med[2] / med[0], reps, st.launches, st.pack_us, st.gpu_us, st.unpack_us,
+           gib / med[2], med[1] / med[0], med[2] / med[0], reps, register_ecmem, st.launches, st.in_place_launches,
+           st.pack_us, st.gpu_us, st.unpack_us,
            same ? "true" : "false");
     reset(&r, nunits);
     for (int p = 0; p < 3; ++p) {
@@ -210,6 +212,9 @@ static int set_bench(int n, int size, int reps) {
     ecm.size = arena;
     ecm.mem = malloc(arena);
     fill(ecm.mem, arena, 5);
+    uint8_t *alias; /* the data process's ecmem registered once, as INTEGRATION §3 sets it up:
+                       the batch reads the old bytes in place */
+    if (register_ecmem && cec_host_register(ecm.mem, arena, &alias)) return fprintf(stderr, "%s\n", cec_last_error()), 2;
     cocytus_set_diff *sd = calloc((size_t)n, sizeof *sd);
     int *perm = malloc(sizeof(int) * (size_t)n);
     for (int e = 0; e < n; ++e) perm[e] = e;
@@ -263,20 +268,23 @@ static int set_bench(int n, int size, int reps) {
     printf("{\"shape\": \"set_diffs\", \"sets\": %d, \"value_bytes\": %d, \"glue_ms\": %.3f, \"glue_GiBps\": %.2f, "
            "\"dropin_loop_ms\": %.1f, \"dropin_loop_GiBps\": %.3f, \"dropin_us_per_set\": %.2f, "
            "\"cpu_restated_1thread_ms\": %.3f, \"cpu_restated_1thread_GiBps\": %.2f, \"glue_vs_dropin\": %.1f, "
-           "\"glue_vs_cpu_1thread\": %.2f, \"last_batch\": {\"launches\": %d, \"rounds\": %d, \"plan_us\": %.0f, "
+           "\"glue_vs_cpu_1thread\": %.2f, \"ecmem_registered\": %d, \"last_batch\": {\"launches\": %d, \"in_place\": %d, \"rounds\": %d, \"plan_us\": %.0f, "
            "\"pack_us\": %.0f, \"gpu_wait_us\": %.0f, \"unpack_us\": %.0f}, \"verified\": %s}\n",
            n, size, 1e3 * med[0], gib / med[0], 1e3 * med[1], gib / med[1], 1e6 * med[1] / n, 1e3 * med[2],
-           gib / med[2], med[1] / med[0], med[2] / med[0], st.launches, st.rounds, st.plan_us, st.pack_us, st.gpu_us,
+           gib / med[2], med[1] / med[0], med[2] / med[0], register_ecmem, st.launches, st.in_place_launches, st.rounds,
+           st.plan_us, st.pack_us, st.gpu_us,
            st.unpack_us, same ? "true" : "false");
     for (int e = 0; e < n; ++e) free((void *)sd[e].value);
     for (int p = 0; p < 3; ++p) free(diffs[p]);
     free(sd);
     free(perm);
+    if (register_ecmem) cec_host_unregister(ecm.mem);
     free(ecm.mem);
     return same ? 0 : 4;
 }
 
 int main(int argc, char **argv) {
+    register_ecmem = !(getenv("RECOVERY_BENCH_STAGED") && atoi(getenv("RECOVERY_BENCH_STAGED")));
     if (argc >= 4 && !strcmp(argv[1], "set")) {
         if (cec_device_check() != CEC_OK) return fprintf(stderr, "%s\n", cec_last_error()), 2;
         const int reps = argc > 4 ? atoi(argv[4]) : 7;
@@ -294,6 +302,9 @@ int main(int argc, char **argv) {
     ecm.size = (uint64_t)nunits * U;
     ecm.mem = malloc(ecm.size);
     fill(ecm.mem, ecm.size, 99);
+    uint8_t *alias; /* the parity's ecmem registered once (the drain needs it so):
+                       the first-touch parity units are then read in place */
+    if (register_ecmem && cec_host_register(ecm.mem, ecm.size, &alias)) return fprintf(stderr, "%s\n", cec_last_error()), 2;
     cocytus_rglue *g;
     if (cocytus_rglue_create(&g, K, M, matrix, SELF, NULL)) return 2;
     int start = 100;
@@ -311,6 +322,7 @@ int main(int argc, char **argv) {
     }
     rc |= shape("idle_85", 85, 1, starts, reps, nunits, &ecm, g);
     cocytus_rglue_destroy(g);
+    if (register_ecmem) cec_host_unregister(ecm.mem);
     free(ecm.mem);
     free(matrix);
     return rc;

@@ -240,3 +240,47 @@ def test_batch_refused_while_capturing(gpu, oracle):
     g.replay()
     torch.cuda.synchronize()
     assert float(x.sum()) == 16.0 and np.array_equal(heap, keep)
+
+
+def test_batch_bases_in_place_from_a_registered_region(gpu, oracle):
+    """Bases inside a region registered with cec_host_register (the server's ecmem) are read
+    in place through its device alias -- recovery's first touch (unit = parity unit ^ c *
+    peer) and SET diffs (diff = old ^ new) -- with the same bytes as the staged path; a
+    round whose bases leave the region, or whose destinations overlap, is staged."""
+    torch, ec = gpu
+    rng = np.random.default_rng(31)
+    heap = rng.integers(0, 256, 16 << 20, dtype=np.uint8)
+    arena = heap[:4 << 20]                       # the registered "ecmem"
+    ec.host_register(arena)
+    try:
+        U = 4096
+        units = [(8 << 20) + int(i) * (U + 80) for i in rng.permutation(256)]
+        jobs = [((5 << 20) + i * U, units[i], int(rng.integers(0, 1000)) * U + 16 * int(rng.integers(0, 4)),
+                 U - 16 * int(rng.integers(0, 2)), 245, 1) for i in range(256)]
+        want = _model(oracle, heap, jobs)
+        _run(ec, heap, jobs)
+        st = ec.batch_stats()
+        assert np.array_equal(heap, want) and st["in_place_launches"] == st["launches"] >= 1
+        # SET diffs: 600 values, old bytes in the registered arena, diffs elsewhere
+        heap[:] = rng.integers(0, 256, heap.size, dtype=np.uint8)
+        jobs, d = [], 9 << 20
+        for _ in range(600):
+            n = int(rng.integers(1, 9000))
+            addr = 16 * int(rng.integers(0, ((4 << 20) - n) // 16))
+            jobs.append(((6 << 20) + int(rng.integers(0, (2 << 20) - n)), d, addr, n, 1, 1))
+            d += n + int(rng.integers(0, 64))
+        want = _model(oracle, heap, jobs)
+        _run(ec, heap, jobs)
+        st = ec.batch_stats()
+        assert np.array_equal(heap, want) and st["in_place_launches"] == st["launches"]
+        # a base outside the region: staged (same bytes)
+        jobs[7] = (jobs[7][0], jobs[7][1], (31 << 19), jobs[7][3], 1, 1)  # past every destination
+        heap[:] = rng.integers(0, 256, heap.size, dtype=np.uint8)
+        want = _model(oracle, heap, jobs)
+        _run(ec, heap, jobs)
+        assert np.array_equal(heap, want) and ec.batch_stats()["in_place_launches"] < ec.batch_stats()["launches"]
+    finally:
+        ec.host_unregister(arena)
+    # unregistered again: staged
+    _run(ec, heap, [((5 << 20), (8 << 20), 0, 4096, 3, 1)])
+    assert ec.batch_stats()["in_place_launches"] == 0
