@@ -171,6 +171,9 @@ _SIGS = {
     "cec_recovery_pool_flush": ([_vp, _vp], _i),
     "cec_recovery_pool_flush_solve": ([_vp, _pp, _vp], _i),
     "cec_recovery_pool_solved": ([_vp, _i], _i),
+    "cec_recovery_pool_flush_solve_host": ([_vp, _vp], _i),
+    "cec_recovery_pool_solve_host": ([_vp, _ip, _i, _vp], _i),
+    "cec_recovery_pool_output": ([_vp, _i, ctypes.POINTER(ctypes.c_size_t)], _vp),
     "cec_recovery_pool_staging": ([_vp, _i, _i, ctypes.POINTER(ctypes.c_size_t)], _vp),
     "cec_recovery_pool_complete": ([_vp, _i], _i),
     "cec_recovery_pool_fold_update": ([_vp, _i, ctypes.c_uint64, _vp, _u32, _vp], _i),
@@ -694,6 +697,28 @@ class RecoveryPool:
         if rc < 0:
             _check(rc)
         return rc
+
+    def flush_solve_host(self, stream=None) -> int:
+        """flush(), also solving every single-loss request it completes into the pool's
+        own host output (read with output())."""
+        rc = lib().cec_recovery_pool_flush_solve_host(self._h, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return rc
+
+    def solve_host(self, rids, stream=None) -> None:
+        ids = (ctypes.c_int * len(rids))(*rids)
+        _check(lib().cec_recovery_pool_solve_host(self._h, ids, len(rids), _stream(stream)))
+
+    def output(self, rid: int):
+        """numpy uint8 view of rid's rebuilt units after a _host solve, or None."""
+        import numpy as np
+
+        n = ctypes.c_size_t()
+        addr = lib().cec_recovery_pool_output(self._h, rid, ctypes.byref(n))
+        if not addr:
+            return None
+        return np.ctypeslib.as_array((ctypes.c_uint8 * n.value).from_address(addr))
 
     def solved(self, rid: int) -> bool:
         return bool(lib().cec_recovery_pool_solved(self._h, rid))

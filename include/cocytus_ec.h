@@ -377,6 +377,9 @@ int cec_recovery_pool_flush(cec_recovery_pool *pool, void *stream);
  * this parity: out[lost lid] (k device arenas by data lid, arena-addressed) =
  * inv * residual.  Returns the requests solved; cec_recovery_pool_solved tells which. */
 int cec_recovery_pool_flush_solve(cec_recovery_pool *pool, uint8_t *const *out, void *stream);
+/* 1 while the request's rebuilt bytes are current: a solve (fused or explicit) wrote them
+ * and no fold_update has changed its residual since (a lost lid's diff, recovery.c:116-120,
+ * clears it). */
 int cec_recovery_pool_solved(const cec_recovery_pool *pool, int id);
 /* check_recovery_1st_completeness: every data lid of the request's mask applied or queued. */
 int cec_recovery_pool_complete(const cec_recovery_pool *pool, int id);
@@ -388,6 +391,16 @@ int cec_recovery_pool_fold_update(cec_recovery_pool *pool, int peer_lid, uint64_
  * inv * residual for every listed complete request, one launch (flushes first). */
 int cec_recovery_pool_solve(cec_recovery_pool *pool, const int *ids, int n, uint8_t *const *out,
                             void *stream);
+/* For a server whose recovery state stays in host memory (integration/
+ * cocytus_recovery_pool.c): the same two solves, but into the pool's own mapped pinned
+ * output at each request's slots instead of an arena, so no unit the caller has not
+ * chosen is written (fill_completed_recovered_data skips sub_flags == 2 units,
+ * memcached.c:7967-8000).  The bytes are fenced for the host when the call returns. */
+int cec_recovery_pool_flush_solve_host(cec_recovery_pool *pool, void *stream);
+int cec_recovery_pool_solve_host(cec_recovery_pool *pool, const int *ids, int n, void *stream);
+/* Request id's rebuilt bytes (*len = its units x 4 KiB) after a _host solve, while
+ * cec_recovery_pool_solved(id) holds; NULL otherwise.  Valid until the request ends. */
+const uint8_t *cec_recovery_pool_output(const cec_recovery_pool *pool, int id, size_t *len);
 /* Non-leader: copy request id's residual (its units x 4 KiB) to dst (host or device). */
 int cec_recovery_pool_residual(cec_recovery_pool *pool, int id, void *dst, void *stream);
 /* recovery_req_remove: release the request's units. */

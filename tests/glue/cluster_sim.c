@@ -6,6 +6,11 @@
  *
  *   cluster_sim SEED [DEFER [CONTROL [NLOST_MAX]]]   (NLOST_MAX: at most this many data lids lost, <= M)
  *
+ * DEFER: 0 the immediate glue calls, 1 the deferred ones (cocytus_recovery.c, both), 2 the pool
+ * placement (cocytus_recovery_pool.c: the residuals in a cec_recovery_pool per parity, replies
+ * copied or received into its staging, the non-leaders' units sent from cocytus_rpool_residual,
+ * the leader's solve at cocytus_rpool_flush; unit->data stays NULL).
+ *
  * CONTROL = 1 breaks the protocol on purpose (a reply applied before its peer's queued diffs
  * are drained): the rebuilt bytes must then differ -- the check has teeth.
  *
@@ -39,6 +44,7 @@
 
 #include "cocytus_drain.h"
 #include "cocytus_recovery.h"
+#include "cocytus_recovery_pool.h"
 #include "cocytus_set.h"
 #include "gf8_ref.h" /* oracle: the final parity check only */
 #include "rep_queue.h"
@@ -71,7 +77,12 @@ struct parity {
     cocytus_rglue *g;
     cocytus_fold_ctx fold;
     cec_drainer *dr;
+    cocytus_rpool *pg; /* DEFER 2 */
+    cocytus_rpool_fold_ctx pfold;
+    struct recovery_queue_item item[1]; /* rec.queue.items: one request in flight */
 };
+
+static int pool_mode;
 
 static int *matrix;
 static struct ecmem data[K];
@@ -91,6 +102,10 @@ static int drain(struct parity *p, int lid, int defer) {
     static cec_host_update scratch[QCAP];
     p->fold.defer = defer;
     cocytus_drain_hooks hooks = {.item_nbytes = item_nbytes, .try_update_batch = cocytus_fold_hook, .ctx = &p->fold};
+    if (pool_mode) {
+        hooks.try_update_batch = cocytus_rpool_fold_hook;
+        hooks.ctx = &p->pfold;
+    }
     const int rc = cocytus_drain_gf(q, lid, p->done[lid], upto, &hooks, p->dr, p->dev, NULL, scratch, QCAP);
     if (rc < 0) {
         fprintf(stderr, "drain: %d %s\n", rc, cec_last_error());
@@ -158,7 +173,8 @@ int main(int argc, char **argv) {
     if (argc < 2) return 1;
     const uint64_t seed = (uint64_t)atoll(argv[1]);
     rng_s = 0x9E3779B97F4A7C15ull ^ seed * 0x2545F4914F6CDD1Dull;
-    const int defer = argc > 2 && atoi(argv[2]);
+    const int defer = argc > 2 ? atoi(argv[2]) : 0;
+    pool_mode = defer == 2;
     const int control = argc > 3 && atoi(argv[3]);
     const int nlost_max = argc > 4 ? atoi(argv[4]) : M;
     if (nlost_max < 1) return 1;
@@ -193,6 +209,14 @@ int main(int argc, char **argv) {
         P->fold.r = &P->rec;
         for (int l = 0; l < K + M; ++l) P->fold.touch_flags[l] = P->touch[l];
         P->fold.sub_flags = NULL;
+        P->rec.queue.items = P->item;
+        P->rec.queue.cap = 1;
+        if (pool_mode && cocytus_rpool_create(&P->pg, K, M, matrix, P->lid, P->dev, 1, 32, NULL))
+            return fprintf(stderr, "rpool: %s\n", cec_last_error()), 2;
+        P->pfold.g = P->pg;
+        P->pfold.r = &P->rec;
+        for (int l = 0; l < K + M; ++l) P->pfold.touch_flags[l] = P->touch[l];
+        P->pfold.sub_flags = NULL;
     }
     /* normal operation: SETs everywhere, drains now and then */
     for (int i = 0; i < 600; ++i) {
@@ -231,6 +255,19 @@ int main(int argc, char **argv) {
         const int span = (int)(rnd() % 24);
         const int ue = ub + span < NU - 1 ? ub + span : NU - 1;
         const size_t nbuf = (size_t)(ue - ub + 1) * U;
+        char *dfp[K + M];
+        memset(dfp, 0, sizeof dfp);
+        for (int q = 0; q < np && pool_mode; ++q) { /* recovery_req_add at each parity of the mask */
+            struct recovery_queue_item *it = &part[q]->item[0];
+            memset(it, 0, sizeof *it);
+            it->unit_begin = ub;
+            it->unit_end = ue;
+            it->mask = mask;
+            it->in_use = 1;
+            it->data_from_parity = dfp;
+            if (cocytus_rpool_begin(part[q]->pg, &part[q]->rec, it))
+                return fprintf(stderr, "begin: %s\n", cec_last_error()), 2;
+        }
         /* replies arrive in a random order, SETs and drains before, between and after */
         int order[K], no = 0;
         for (int j = 0; j < K; ++j)
@@ -254,6 +291,15 @@ int main(int argc, char **argv) {
             for (int q = 0; q < np; ++q) { /* each parity of the mask gets the reply */
                 struct parity *P = part[q];
                 if (!control) drain(P, peer, defer); /* recover_units_reply: the peer's xids first (:4311-4316) */
+                if (pool_mode) { /* received into the pool's staging, or copied in from c->vbuf */
+                    char *st = rnd() % 2 ? cocytus_rpool_staging(P->pg, &P->rec, &P->item[0], peer) : NULL;
+                    char *reply = st ? st : malloc(nbuf);
+                    memcpy(reply, (char *)data[peer].mem + (size_t)ub * U, nbuf);
+                    const int rc = cocytus_rpool_recover_units(P->pg, &P->rec, &P->item[0], peer, reply);
+                    if (!st) free(reply);
+                    if (rc) return fprintf(stderr, "recover: %d %s\n", rc, cec_last_error()), 2;
+                    continue;
+                }
                 char *reply = malloc(nbuf);
                 memcpy(reply, (char *)data[peer].mem + (size_t)ub * U, nbuf);
                 const int rc = defer ? cocytus_recover_units_defer(P->g, &P->rec, &P->ecm, peer, ub, ue, reply, 1)
@@ -262,13 +308,39 @@ int main(int argc, char **argv) {
                 if (rc) return fprintf(stderr, "recover: %d %s\n", rc, cec_last_error()), 2;
             }
         }
+        if (pool_mode) { /* non-leaders send their residuals, the leader solves at its flush */
+            for (int q = 0; q < np; ++q) {
+                struct parity *P = part[q];
+                if (P == L) continue;
+                dfp[P->lid] = malloc(nbuf);
+                if (cocytus_rpool_residual(P->pg, &P->rec, &P->item[0], dfp[P->lid]))
+                    return fprintf(stderr, "residual: %s\n", cec_last_error()), 2;
+            }
+            int n = 0;
+            if (cocytus_rpool_solve(L->pg, &L->rec, &L->item[0], &n) || n != nl || cocytus_rpool_flush(L->pg) != 1)
+                return fprintf(stderr, "solve: n %d of %d: %s\n", n, nl, cec_last_error()), 2;
+            for (int x = 0; x < n; ++x) {
+                const char *d = cocytus_rpool_data(L->pg, &L->rec, &L->item[0], x);
+                if ((!d || memcmp(d, (char *)data[lost[x]].mem + (size_t)ub * U, nbuf)) && !bad) {
+                    printf("range [%d, %d]: rebuilt bytes of lid %d differ from the lost shard\n", ub, ue, lost[x]);
+                    bad = 1;
+                }
+            }
+            for (int l = 0; l < K + M; ++l) free(dfp[l]);
+            for (int q = 0; q < np; ++q) { /* recovery_req_remove: the glue first (recovery.c:196-205) */
+                if (cocytus_rpool_end(part[q]->pg, &part[q]->rec, &part[q]->item[0]))
+                    return fprintf(stderr, "end: %s\n", cec_last_error()), 2;
+                for (int i = ub; i <= ue; ++i) part[q]->rec.units[i].flags = 0;
+            }
+            ranges++;
+            ub = ue + 1;
+            continue;
+        }
         struct recovery_queue_item it;
         memset(&it, 0, sizeof it);
         it.unit_begin = ub;
         it.unit_end = ue;
         it.mask = mask;
-        char *dfp[K + M];
-        memset(dfp, 0, sizeof dfp);
         it.data_from_parity = dfp;
         for (int q = 0; q < np; ++q) {
             struct parity *P = part[q];
@@ -314,6 +386,7 @@ int main(int argc, char **argv) {
     for (int j = 0; j < K; ++j) cec_host_unregister(data[j].mem);
     for (int p = 0; p < M; ++p) {
         cocytus_rglue_destroy(par[p].g);
+        cocytus_rpool_destroy(par[p].pg);
         cec_drainer_destroy(par[p].dr);
         cec_host_unregister(par[p].ecm.mem);
     }

@@ -25,6 +25,14 @@
  * Paths, all from the same inputs, outputs compared byte for byte:
  *   glue        cocytus_recover_units_gf x peers + cocytus_recovery_solve_gf (range), or
  *               every reply and solve deferred and ONE cocytus_recovery_flush (idle);
+ *   pool        the pool placement (integration/cocytus_recovery_pool.c): every request
+ *               begun, every reply copied into the pool's staging, every solve queued, ONE
+ *               cocytus_rpool_flush (one launch); fill_completed_recovered_data then reads
+ *               the rebuilt bytes in place in the pool's mapped output, as it reads the other
+ *               paths' data[] (that memcpy and recovery_req_remove are untimed in every path);
+ *   pool_recv_in_staging  the same with every reply received straight into the pool's
+ *               staging (cocytus_rpool_staging as c->ritem): the recv, like every other
+ *               path's recv into c->vbuf, is not timed, so no copy is;
  *   dropin      the reference's loops as the unchanged server runs them on the shim: one
  *               synchronous galois_w08_region_multiply per unit (and per solve term);
  *   cpu         the same loops on the restated CPU region multiply (oracle: GF-Complete's
@@ -40,6 +48,7 @@
 #include <cocytus_ec.h>
 
 #include "cocytus_recovery.h"
+#include "cocytus_recovery_pool.h"
 #include "cocytus_set.h"
 #include "gf8_ref.h" /* oracle: the restated CPU region multiply (baseline only) */
 
@@ -116,7 +125,7 @@ static void fill(char *p, size_t n, uint64_t seed) {
 
 /* One shape: nreq requests of `units` units each at unit starts[q]. */
 static int shape(const char *name, int nreq, int units, const int *starts, int reps, int nunits, struct ecmem *ecm,
-                 cocytus_rglue *g) {
+                 cocytus_rglue *g, const uint8_t *alias) {
     const int peers[2] = {0, 2}, lost = 1;
     const uint32_t mask = (1u << SELF) | (1u << 0) | (1u << 2);
     const int inv = galois_single_divide(1, MAT(SELF, lost), 8);
@@ -129,12 +138,19 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
         reply[x] = malloc(nbuf);
         fill(reply[x], nbuf, 0x1234567ull + (uint64_t)x);
     }
-    char **out[3];
-    for (int p = 0; p < 3; ++p) out[p] = calloc((size_t)nreq, sizeof(char *));
-    double t[3][64];
+    char **out[5];
+    for (int p = 0; p < 5; ++p) out[p] = calloc((size_t)nreq, sizeof(char *));
+    const char **pdata = calloc((size_t)nreq, sizeof *pdata);
+    double t[5][64];
     struct recovery_queue_item *it = calloc((size_t)nreq, sizeof *it);
     for (int q = 0; q < nreq; ++q) it[q].mask = mask;
-    for (int path = 0; path < 3; ++path) {
+    r.queue.items = it; /* the requests' keys in the pool placement */
+    r.queue.cap = nreq;
+    cocytus_rpool *pg = NULL; /* needs the arena's device view: a registered ecmem */
+    if (alias && cocytus_rpool_create(&pg, K, M, matrix, SELF, alias, nreq, nreq * units, NULL))
+        return fprintf(stderr, "rpool: %s\n", cec_last_error()), 2;
+    const int npath = pg ? 5 : 3;
+    for (int path = 0; path < npath; ++path) {
         for (int rep = 0; rep <= reps; ++rep) { /* rep 0: warm-up */
             reset(&r, nunits);
             for (int q = 0; q < nreq; ++q) free(out[path][q]);
@@ -144,7 +160,15 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
                 it[q].unit_begin = starts[q] + rep * kRepStride;
                 it[q].unit_end = it[q].unit_begin + units - 1;
             }
+            if (path == 4) { /* the recv: each reply read into the pool's staging (c->ritem), untimed
+                                as every other path's recv into c->vbuf */
+                for (int q = 0; q < nreq; ++q)
+                    if (cocytus_rpool_begin(pg, &r, &it[q])) return fprintf(stderr, "begin: %s\n", cec_last_error()), 2;
+                for (int q = 0; q < nreq; ++q)
+                    for (int p = 0; p < 2; ++p) memcpy(cocytus_rpool_staging(pg, &r, &it[q], peers[p]), reply[2 * q + p], nbuf);
+            }
             const double t0 = now_s();
+            double t_end = 0;
             if (path == 0) {
                 for (int q = 0; q < nreq; ++q)
                     for (int p = 0; p < 2; ++p) {
@@ -164,6 +188,32 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
                 }
                 if (nreq > 1 && cocytus_recovery_flush(g) != 3 * nreq)
                     return fprintf(stderr, "flush: %s\n", cec_last_error()), 2;
+            } else if (path >= 3) {
+                if (path == 3)
+                    for (int q = 0; q < nreq; ++q)
+                        if (cocytus_rpool_begin(pg, &r, &it[q]))
+                            return fprintf(stderr, "begin: %s\n", cec_last_error()), 2;
+                for (int q = 0; q < nreq; ++q)
+                    for (int p = 0; p < 2; ++p) {
+                        const char *src = path == 3 ? reply[2 * q + p] : cocytus_rpool_staging(pg, &r, &it[q], peers[p]);
+                        if (cocytus_rpool_recover_units(pg, &r, &it[q], peers[p], src))
+                            return fprintf(stderr, "reply: %s\n", cec_last_error()), 2;
+                    }
+                for (int q = 0; q < nreq; ++q) {
+                    int n = 0;
+                    if (cocytus_rpool_solve(pg, &r, &it[q], &n) || n != 1)
+                        return fprintf(stderr, "solve: %s\n", cec_last_error()), 2;
+                }
+                if (cocytus_rpool_flush(pg) != nreq) return fprintf(stderr, "flush: %s\n", cec_last_error()), 2;
+                for (int q = 0; q < nreq; ++q) pdata[q] = cocytus_rpool_data(pg, &r, &it[q], 0);
+                t_end = now_s(); /* fill_completed_recovered_data reads data in place from here on, as it
+                                    reads the other paths' data[] */
+                for (int q = 0; q < nreq; ++q) {
+                    out[path][q] = malloc(nbuf);
+                    memcpy(out[path][q], pdata[q], nbuf);
+                    cocytus_rpool_end(pg, &r, &it[q]); /* recovery_req_remove (untimed in every path) */
+                    for (int i = it[q].unit_begin; i <= it[q].unit_end; ++i) r.units[i].flags = 0;
+                }
             } else {
                 const mul_fn mul = path == 1 ? mul_dropin : mul_cpu;
                 for (int q = 0; q < nreq; ++q)
@@ -171,33 +221,41 @@ static int shape(const char *name, int nreq, int units, const int *starts, int r
                         ref_recover(&r, ecm, peers[p], it[q].unit_begin, it[q].unit_end, reply[2 * q + p], mul);
                 for (int q = 0; q < nreq; ++q) out[path][q] = ref_solve(&r, it[q].unit_begin, it[q].unit_end, inv, mul);
             }
-            if (rep) t[path][rep - 1] = now_s() - t0;
+            if (rep) t[path][rep - 1] = (path >= 3 ? t_end : now_s()) - t0;
         }
         qsort(t[path], (size_t)reps, sizeof(double), cmp_d);
     }
     int same = 1;
     for (int q = 0; q < nreq; ++q)
-        same &= !memcmp(out[0][q], out[1][q], nbuf) && !memcmp(out[0][q], out[2][q], nbuf);
+        same &= !memcmp(out[0][q], out[1][q], nbuf) && !memcmp(out[0][q], out[2][q], nbuf) &&
+                (!pg || (!memcmp(out[0][q], out[3][q], nbuf) && !memcmp(out[0][q], out[4][q], nbuf)));
     /* payload: the replies folded + the bytes rebuilt */
     const double bytes = (double)nreq * (double)nbuf * 3.0, gib = bytes / (double)(1u << 30);
-    const double med[3] = {t[0][reps / 2], t[1][reps / 2], t[2][reps / 2]};
+    const double med[5] = {t[0][reps / 2], t[1][reps / 2], t[2][reps / 2], pg ? t[3][reps / 2] : 0.0,
+                           pg ? t[4][reps / 2] : 0.0};
     cec_batch_stats st;
     cec_region_multiply_batch_stats(&st);
     printf("{\"shape\": \"%s\", \"requests\": %d, \"units_per_request\": %d, \"code\": \"RS(3,2), leader P1, D1 lost\", "
            "\"payload_MiB\": %.3f, \"glue_us\": %.1f, \"glue_GiBps\": %.3f, \"dropin_loop_us\": %.1f, "
            "\"dropin_loop_GiBps\": %.3f, \"cpu_restated_1thread_us\": %.1f, \"cpu_restated_1thread_GiBps\": %.3f, "
-           "\"glue_vs_dropin\": %.1f, \"glue_vs_cpu_1thread\": %.2f, \"reps\": %d, "
+           "\"glue_vs_dropin\": %.1f, \"glue_vs_cpu_1thread\": %.2f, \"pool_us\": %.1f, \"pool_GiBps\": %.3f, "
+           "\"pool_vs_cpu_1thread\": %.2f, \"pool_vs_glue\": %.2f, \"pool_recv_in_staging_us\": %.1f, "
+           "\"pool_recv_in_staging_GiBps\": %.3f, \"pool_recv_in_staging_vs_cpu_1thread\": %.2f, \"reps\": %d, "
            "\"ecmem_registered\": %d, \"last_batch\": {\"launches\": %d, \"in_place\": %d, \"pack_us\": %.1f, \"gpu_us\": %.1f, \"unpack_us\": %.1f}, "
            "\"verified\": %s}\n",
            name, nreq, units, bytes / (1 << 20), 1e6 * med[0], gib / med[0], 1e6 * med[1], gib / med[1], 1e6 * med[2],
-           gib / med[2], med[1] / med[0], med[2] / med[0], reps, register_ecmem, st.launches, st.in_place_launches,
+           gib / med[2], med[1] / med[0], med[2] / med[0], 1e6 * med[3], pg ? gib / med[3] : 0.0,
+           pg ? med[2] / med[3] : 0.0, pg ? med[0] / med[3] : 0.0, 1e6 * med[4], pg ? gib / med[4] : 0.0,
+           pg ? med[2] / med[4] : 0.0, reps, register_ecmem, st.launches, st.in_place_launches,
            st.pack_us, st.gpu_us, st.unpack_us,
            same ? "true" : "false");
     reset(&r, nunits);
-    for (int p = 0; p < 3; ++p) {
+    cocytus_rpool_destroy(pg);
+    for (int p = 0; p < 5; ++p) {
         for (int q = 0; q < nreq; ++q) free(out[p][q]);
         free(out[p]);
     }
+    free(pdata);
     for (int x = 0; x < 2 * nreq; ++x) free(reply[x]);
     free(reply);
     free(it);
@@ -308,7 +366,8 @@ int main(int argc, char **argv) {
     cocytus_rglue *g;
     if (cocytus_rglue_create(&g, K, M, matrix, SELF, NULL)) return 2;
     int start = 100;
-    int rc = shape("range_1MiB", 1, 256, &start, reps, nunits, &ecm, g);
+    const uint8_t *dev_view = register_ecmem ? alias : NULL;
+    int rc = shape("range_1MiB", 1, 256, &start, reps, nunits, &ecm, g, dev_view);
     int starts[85];
     uint64_t s = 77;
     for (int q = 0; q < 85; ++q) { /* distinct scattered units */
@@ -320,7 +379,7 @@ int main(int argc, char **argv) {
             for (int x = 0; x < q; ++x) ok &= starts[x] != starts[q];
         } while (!ok);
     }
-    rc |= shape("idle_85", 85, 1, starts, reps, nunits, &ecm, g);
+    rc |= shape("idle_85", 85, 1, starts, reps, nunits, &ecm, g, dev_view);
     cocytus_rglue_destroy(g);
     if (register_ecmem) cec_host_unregister(ecm.mem);
     free(ecm.mem);

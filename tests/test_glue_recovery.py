@@ -503,7 +503,7 @@ SIM = os.path.join(ROOT, "oracle", "_ref", "glue_cluster_sim")
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("seed", range(6))
-@pytest.mark.parametrize("defer", [0, 1])
+@pytest.mark.parametrize("defer", [0, 1, 2])
 @pytest.mark.parametrize("code", ["", "63"])
 def test_cluster_sim_rebuilds_the_lost_shard(gpu, seed, defer, code):
     """An RS(3,2) group in one process through all the glue (tests/glue/cluster_sim.c): SET
@@ -511,7 +511,8 @@ def test_cluster_sim_rebuilds_the_lost_shard(gpu, seed, defer, code):
     fold hook into registered host arenas; a data process lost mid-stream; the leader
     parity rebuilds every unit range while the survivors keep writing (each reply applied
     after that peer's queue is drained, drains folding at random moments, immediate or
-    deferred).  RS(3,2) and RS(6,3) (code "63"), 1..M data lids lost: every parity of
+    deferred, or -- defer 2 -- on the pool placement, cocytus_recovery_pool.c).  RS(3,2)
+    and RS(6,3) (code "63"), 1..M data lids lost: every parity of
     start_recovery's mask folds the replies and the non-leaders ship their units to the
     leader (data_from_parity).  Every rebuilt range equals the bytes the lost shards held --
     a truth that needs no oracle -- and the parities end as the code of the data."""
@@ -525,11 +526,12 @@ def test_cluster_sim_rebuilds_the_lost_shard(gpu, seed, defer, code):
 
 
 @pytest.mark.gpu
-def test_cluster_sim_control_breaks_without_the_drain(gpu):
+@pytest.mark.parametrize("defer", [0, 2])
+def test_cluster_sim_control_breaks_without_the_drain(gpu, defer):
     """The same simulation with the protocol broken on purpose -- each reply applied before
     that peer's queued diffs are drained (skipping recover_units_reply's drain,
     memcached.c:4311-4316) -- must rebuild wrong bytes: the check above detects a wrong fold."""
     if not os.path.exists(SIM):
         pytest.skip("oracle/_ref/glue_cluster_sim not built (make -C oracle ref)")
-    r = subprocess.run([SIM, "0", "0", "1", "1"], capture_output=True, text=True, timeout=300)
+    r = subprocess.run([SIM, "0", str(defer), "1", "1"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 1 and "differ" in r.stdout, r.stdout + r.stderr

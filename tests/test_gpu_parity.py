@@ -1469,15 +1469,19 @@ def test_recovery_finish_rejects_early_peer(gpu, oracle):
 
 # ------------------------------------------------------------------ recovery pool (§8f 2)
 @pytest.mark.parametrize("engine_name", ["perm", "lds"])
-@pytest.mark.parametrize("out_kind", ["device", "pinned"])
+@pytest.mark.parametrize("out_kind", ["device", "pinned", "host"])
 def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
     """The idle recoverer's traffic (memcached.c:5712-5734): single-unit and short-range
     requests, a bounded window in flight, replies from D1 / D2 in random order, flushes at
-    random points, SETs on D1 / D2 landing mid-recovery (fold_update, then the parity
-    apply, memcached.c:7757-7764), batched leader solves.  Every rebuilt unit of lost D0
-    equals the live data.  With `pinned`, the rebuilt shard's arena is pinned host memory
-    and is read as soon as the last synchronous solve returns (no device sync): the pool
-    then waits with the system-fence event."""
+    random points, SETs landing mid-recovery (fold_update, then the parity apply,
+    memcached.c:7757-7764) on D1 / D2 and on lost D0 (its substitute forwards them under
+    lid 0, which recovery.c:116-120 folds like any other), batched leader solves.  Every
+    rebuilt unit of lost D0 equals the live data.  With `pinned`, the rebuilt shard's arena
+    is pinned host memory and is read as soon as the last synchronous solve returns (no
+    device sync): the pool then waits with the system-fence event.  With
+    `host`, the rebuilt shard is a pageable host array (the unchanged server's sub_ecmem)
+    and the solves go to the pool's own output (the _host calls), copied out per request
+    as fill_completed_recovered_data does (memcached.c:7967-8000)."""
     torch, ec = gpu
     default = ec.get_engine()
     ec.set_engine(ec.CEC_ENGINE_PERM if engine_name == "perm" else ec.CEC_ENGINE_LDS)
@@ -1488,14 +1492,36 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
         nunits = 256
         data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
         p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
-        out0 = (torch.zeros(nunits * U, dtype=torch.uint8).pin_memory() if out_kind == "pinned"
+        host = out_kind == "host"
+        out0 = (np.zeros(nunits * U, dtype=np.uint8) if host
+                else torch.zeros(nunits * U, dtype=torch.uint8).pin_memory() if out_kind == "pinned"
                 else torch.zeros(nunits * U, dtype=torch.uint8, device="cuda"))
         mask = oracle.recovery_mask(k, m, 3, [0, 1, 1, 1, 1])  # D0 lost, leader P0
         pending, done = {}, []  # id -> (ub, ue, peers left)
+        ranges, rebuilt = {}, np.zeros(nunits, dtype=bool)  # id -> (ub, ue); units solved into out0
+
+        def mark_solved():
+            for i, (a, b) in ranges.items():
+                if pool.solved(i):
+                    rebuilt[a:b + 1] = True
+                    if host:  # fill_completed_recovered_data from the pool's output
+                        out0[a * U:(b + 1) * U] = pool.output(i)
+
+        def flush_solve():
+            if host:
+                pool.flush_solve_host()
+            else:
+                pool.flush_solve([out0, None, None])
+
+        def solve(ids):
+            if host:
+                pool.solve_host(ids)
+            else:
+                pool.solve(ids, [out0, None, None])
 
         def check_sync():  # a solve into pinned memory is fenced before it returns; HBM: not
             sync = ec.last_sync()
-            want = (1, 1) if out_kind == "pinned" else (0, 0)
+            want = (0, 0) if out_kind == "device" else (1, 1)
             assert (sync["host_results"], sync["fenced"]) == want, (out_kind, sync)
 
         next_unit, window = 0, 24
@@ -1505,7 +1531,8 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                     n = 1 if rng.random() < 0.7 else int(rng.integers(2, 5))
                     ub, ue = next_unit, min(nunits - 1, next_unit + n - 1)
                     try:
-                        pending[pool.begin(mask, ub, ue)] = (ub, ue, [1, 2])
+                        i = pool.begin(mask, ub, ue)
+                        pending[i], ranges[i] = (ub, ue, [1, 2]), (ub, ue)
                     except ec.CecError as e:  # pool full: back off like the TOO_MANY check
                         assert e.code == ec.CEC_EFULL
                         break
@@ -1523,10 +1550,12 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                     if rng.random() < 0.5:
                         pool.flush()
                     else:  # the completed single-loss requests are rebuilt in the same pass
-                        pool.flush_solve([out0, None, None])
+                        flush_solve()
                         check_sync()
-                if rng.random() < 0.25:  # a SET on a surviving data shard lands
-                    j = int(rng.integers(1, 3))
+                        mark_solved()
+                if rng.random() < 0.25:  # a SET lands: on D1 / D2, or on lost D0 through its
+                    # substitute, forwarded under lid 0 (memcached.c:7700, :7758)
+                    j = int(rng.integers(0, 3))
                     ln = int(rng.integers(1, 9000))
                     addr = int(rng.integers(0, nunits * U - ln)) // 16 * 16
                     new = rng.integers(0, 256, ln, dtype=np.uint8)
@@ -1534,25 +1563,37 @@ def test_recovery_pool_idle_recoverer(gpu, oracle, engine_name, out_kind):
                     data[j][addr:addr + ln] = new
                     pool.fold_update(j, addr, diff)
                     ec.region_multiply(to_dev(torch, diff), mat[3 * k + j], ln, p0.data_ptr() + addr, 1)
+                    if j == 0:  # units already rebuilt: the substitute writes them itself
+                        for u in range(addr // U, (addr + ln - 1) // U + 1):
+                            if rebuilt[u]:
+                                lo, hi = max(addr, u * U), min(addr + ln, (u + 1) * U)
+                                out0[lo:hi] = (data[0][lo:hi] if host else
+                                               torch.from_numpy(data[0][lo:hi].copy()).to(out0.device))
                     torch.cuda.synchronize()
                 if not left:
                     assert pool.complete(rid)
                     del pending[rid]
                     if pool.solved(rid):
                         pool.end(rid)
+                        del ranges[rid]
                     else:
                         done.append(rid)
                 if done and (rng.random() < 0.3 or not pending):
-                    pool.solve(done, [out0, None, None])
+                    solve(done)
                     check_sync()
                     for d in done:
+                        assert pool.solved(d)
+                        a, b = ranges.pop(d)
+                        rebuilt[a:b + 1] = True
+                        if host:
+                            out0[a * U:(b + 1) * U] = pool.output(d)
                         pool.end(d)
                     done = []
             assert pool.active == 0
             if out_kind == "pinned":  # read on return of the last synchronous call
                 assert np.array_equal(out0.numpy(), data[0])
         torch.cuda.synchronize()
-        assert np.array_equal(to_host(out0), data[0])
+        assert np.array_equal(out0 if host else to_host(out0), data[0])
     finally:
         ec.set_engine(default)
 

@@ -54,7 +54,7 @@ run)
         -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
     timeout -k 10 200 "$A/glue_recovery_bench" 3
     timeout -k 10 200 "$A/glue_recovery_bench" set 16384 4098 2
-    for s in 0 1 2; do timeout -k 10 200 "$A/glue_cluster_sim63" $s $((s % 2)); done
+    for s in 0 1 2; do timeout -k 10 200 "$A/glue_cluster_sim63" $s $s; done
   fi
   ;;
 glue)  # (here, on the CPU, where the reference's headers are) the glue programs against tools/asan
@@ -70,6 +70,7 @@ glue)  # (here, on the CPU, where the reference's headers are) the glue programs
       -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_recovery_bench" \
       "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_set.c" \
+      "$R/integration/cocytus_recovery_pool.c" \
       -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
   ;;
 *) echo "usage: $0 build|glue|run" >&2; exit 2 ;;

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-5 GPU calls (run on the box by gpurun from the repo root).  Usage: bash tools/r05_calls.sh <case>
 #   d  host batch + glue tests, the glue benches (recovery, SET diffs, drain in both placements)
+#   i  the recovery glue's pool placement (tests + bench)
 set -o pipefail
 case "$1" in
 d)
@@ -40,6 +41,12 @@ h)  # where the host batch's GPU time goes: kernel durations of the recovery sha
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 200 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$out/prof" -o run --output-format csv \
         -- python3 "$GRAFT_REPO_ROOT/tools/hostbatch_bench.py" 5 > $out/hostbatch_bench.jsonl 2> $out/err.log
+    ;;
+i)  # the pool placement of the recovery glue: its tests, the pool's own tests, the bench shapes
+    out=gpurun_out/r05i; mkdir -p $out
+    timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_glue_rpool.py \
+        tests/test_gpu_parity.py tests/test_glue_recovery.py -k "rpool or recovery_pool or cluster_sim" > $out/pytest.log 2>&1 || exit 1
+    timeout -k 10 120 oracle/_ref/glue_recovery_bench 15 > $out/recovery_bench.jsonl 2>&1 || exit 2
     ;;
 *) echo "unknown case $1"; exit 9 ;;
 esac

@@ -37,7 +37,7 @@ glue)  # (here, on the CPU) the glue bench against tools/tsan
   RT=$ROCM/lib/llvm/lib/clang/22/lib/linux
   $ROCM/llvm/bin/clang -O1 -g -std=gnu11 -fsanitize=thread -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" \
       -o "$T/glue_recovery_bench" "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" \
-      "$R/integration/cocytus_set.c" -L"$T" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
+      "$R/integration/cocytus_set.c" "$R/integration/cocytus_recovery_pool.c" -L"$T" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
       -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,--whole-archive $RT/libclang_rt.tsan_cxx-x86_64.a -Wl,--no-whole-archive -lstdc++
   ;;
 *) echo "usage: $0 build|glue|run" >&2; exit 2 ;;
