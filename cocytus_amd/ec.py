@@ -177,6 +177,7 @@ _SIGS = {
     "cec_recovery_pool_staging": ([_vp, _i, _i, ctypes.POINTER(ctypes.c_size_t)], _vp),
     "cec_recovery_pool_complete": ([_vp, _i], _i),
     "cec_recovery_pool_fold_update": ([_vp, _i, ctypes.c_uint64, _vp, _u32, _vp], _i),
+    "cec_recovery_pool_fold_updates": ([_vp, _vp, _i, _ip, _vp], _i),
     "cec_recovery_pool_solve": ([_vp, _ip, _i, _pp, _vp], _i),
     "cec_recovery_pool_residual": ([_vp, _i, _vp, _vp], _i),
     "cec_recovery_pool_end": ([_vp, _i], _i),
@@ -732,6 +733,16 @@ class RecoveryPool:
         if rc < 0:
             _check(rc)
         return rc
+
+    def fold_updates(self, updates, stream=None):
+        """updates: [(host diff, addr, peer_lid)] (host_updates' form), one drain window,
+        folded as fold_update per update.  Returns the units folded per update."""
+        arr = host_updates(updates) if updates else (HostUpdate * 1)()
+        units = (ctypes.c_int * max(len(updates), 1))()
+        rc = lib().cec_recovery_pool_fold_updates(self._h, arr, len(updates), units, _stream(stream))
+        if rc < 0:
+            _check(rc)
+        return [units[i] for i in range(len(updates))]
 
     def solve(self, rids, out_arenas, stream=None) -> None:
         """out_arenas: k device arenas by data lid (None where not lost)."""

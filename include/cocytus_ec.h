@@ -387,6 +387,11 @@ int cec_recovery_pool_complete(const cec_recovery_pool *pool, int id);
  * units folded (>= 0) or a negative cec_status. */
 int cec_recovery_pool_fold_update(cec_recovery_pool *pool, int peer_lid, uint64_t addr, const void *diff,
                                   uint32_t len, void *stream);
+/* The same for a drain window: every update u[i] (host buffers; any data lid) folded as
+ * cec_recovery_pool_fold_update would fold it, in one upload and one launch per overlap
+ * wave (flushes first).  units[i] (optional) = update i's units folded; returns their sum. */
+int cec_recovery_pool_fold_updates(cec_recovery_pool *pool, const cec_host_update *u, int n, int *units,
+                                   void *stream);
 /* Leader, single loss: out[lost lid] (k device arenas by data lid, arena-addressed) =
  * inv * residual for every listed complete request, one launch (flushes first). */
 int cec_recovery_pool_solve(cec_recovery_pool *pool, const int *ids, int n, uint8_t *const *out,

@@ -45,6 +45,10 @@ struct cocytus_rpool {
     int n_want;
     cec_region_job *jobs;
     int cap_jobs;
+    cec_host_update *win; /* a drain window's updates that fold */
+    int cap_win;
+    int *win_units; /* [units folded per update | units expected] */
+    int cap_win_units;
 };
 
 static int grow(void **p, int *cap, int need, size_t elem) {
@@ -102,6 +106,8 @@ void cocytus_rpool_destroy(cocytus_rpool *g) {
         for (int i = 0; i < g->qcap; ++i) free_own(&g->q[i]);
     if (g->pool) cec_recovery_pool_destroy(g->pool);
     free(g->jobs);
+    free(g->win);
+    free(g->win_units);
     free(g->want);
     free(g->q);
     free(g->matrix);
@@ -230,14 +236,33 @@ int cocytus_rpool_try_update_units(cocytus_rpool *g, struct recovery *r, char *c
     if (!g || !r || !r->units || n < 0 || (n && (!u || !need))) return CEC_EINVAL;
     for (int i = 0; i < n; ++i)
         if (u[i].src_lid >= (uint32_t)g->k || (u[i].len && !u[i].buf)) return CEC_EINVAL;
-    for (int i = 0; i < n; ++i) { /* in xid order: each fold as process_rep_command makes it */
+    /* the walks in xid order (the flags do not change within the window), then every fold of
+     * the window in one pool call: the applies come after the whole window, so one flush of
+     * the queued first touches ahead of them is enough */
+    int rc, nf = 0, any_upd = 0;
+    if ((rc = grow((void **)&g->win, &g->cap_win, n, sizeof *g->win)) ||
+        (rc = grow((void **)&g->win_units, &g->cap_win_units, 2 * n, sizeof *g->win_units)))
+        return rc;
+    int *want = g->win_units + n;
+    for (int i = 0; i < n; ++i) {
         const int lid = (int)u[i].src_lid;
         int nfold, nupd;
         need[i] = walk(g, r, touch_flags ? touch_flags[lid] : NULL, sub_flags, lid, u[i].addr, u[i].len, &nfold,
                        &nupd);
-        const int rc = fold(g, lid, u[i].addr, (const char *)u[i].buf, u[i].len, nfold, nupd);
-        if (rc) return rc;
+        any_upd |= nupd > 0;
+        if (nfold) {
+            g->win[nf] = u[i];
+            want[nf++] = nfold;
+        }
     }
+    if (!nf) {
+        rc = any_upd ? cec_recovery_pool_flush(g->pool, g->stream) : CEC_OK;
+        return rc < 0 ? rc : CEC_OK;
+    }
+    rc = cec_recovery_pool_fold_updates(g->pool, g->win, nf, g->win_units, g->stream);
+    if (rc < 0) return rc;
+    for (int i = 0; i < nf; ++i)
+        if (g->win_units[i] != want[i]) return CEC_EINVAL; /* the pool's requests and the flags disagree */
     return CEC_OK;
 }
 

@@ -1632,6 +1632,55 @@ def test_recovery_pool_non_leader_residual_and_errors(gpu, oracle):
         assert pool.begin(0b11100, 10, 17) >= 0  # room again
 
 
+@pytest.mark.parametrize("capacity", [64, 12])
+def test_recovery_pool_fold_updates_window(gpu, oracle, capacity):
+    """A drain window folded at once (cec_recovery_pool_fold_updates) equals the same
+    updates folded one by one (cec_recovery_pool_fold_update, recovery.c:99-131) on a twin
+    pool: 300 SET diffs of every data lid -- lost ones too -- crowded onto few units, so
+    they meet in R and split into waves; requests untouched, touched, complete and
+    partly fed.  capacity 12: the window has more tiles than the pool's tile buffer."""
+    torch, ec = gpu
+    k, m, U = 4, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xF01D + capacity)
+    nunits = 64
+    data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+    p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
+    mask = 0b010000 | 0b1110  # D0 lost, leader P0
+    pools = [ec.RecoveryPool(k, m, mat, 4, p0, capacity_units=capacity) for _ in range(2)]
+    try:
+        ranges = [(2, 2), (3, 5), (8, 8), (9, 10), (20, 22)]
+        rids = []
+        for x, (ub, ue) in enumerate(ranges):
+            ids = [pl.begin(mask, ub, ue) for pl in pools]
+            assert ids[0] == ids[1]
+            rids.append(ids[0])
+            for j in [1, 2, 3][:x % 4]:  # 0..3 peers fed: untouched, partly fed, complete
+                for pl in pools:
+                    pl.add_peer(ids[0], j, data[j][ub * U:(ue + 1) * U].copy())
+        window = []
+        for _ in range(300):
+            ln = int(rng.integers(1, 3 * U))
+            addr = int(rng.integers(1 * U, 12 * U - ln)) if rng.random() < 0.8 else \
+                int(rng.integers(0, nunits * U - ln))
+            window.append((rng.integers(0, 256, ln, dtype=np.uint8), addr, int(rng.integers(0, k))))
+        got = pools[0].fold_updates(window)
+        want = [pools[1].fold_update(lid, addr, diff) for diff, addr, lid in window]
+        assert got == want
+        assert sum(got) > 60, "the window should mostly land on units under recovery"
+        for x, (rid, (ub, ue)) in enumerate(zip(rids, ranges)):
+            if x % 4 == 0:  # untouched: no residual yet (both pools fold nothing into it)
+                continue
+            a, b = np.zeros((ue - ub + 1) * U, np.uint8), np.zeros((ue - ub + 1) * U, np.uint8)
+            pools[0].residual(rid, a)
+            pools[1].residual(rid, b)
+            assert np.array_equal(a, b), (ub, ue)
+        assert pools[0].fold_updates([]) == []
+    finally:
+        for pl in pools:
+            pl.destroy()
+
+
 def test_batched_bindings_c_program(gpu, oracle, tmp_path):
     """The batched bindings from a C99 program (cec_encode_region, cec_diff_update,
     cec_drainer_apply, cec_recovery_pool) vs the reference's chains."""

@@ -50,8 +50,9 @@ run)
   # against the reference's headers on the CPU (glue build, below) and linked here to the
   # instrumented library: the GPU glue tests through that binary, then its bench shapes
   if [ -x "$A/glue_recovery" ]; then
-    CEC_GLUE_RECOVERY_EXE="$A/glue_recovery" timeout -k 10 300 python -u -m pytest tests/test_glue_recovery.py \
-        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider
+    CEC_GLUE_RECOVERY_EXE="$A/glue_recovery" CEC_GLUE_RPOOL_EXE="$A/glue_rpool" timeout -k 10 300 \
+        python -u -m pytest tests/test_glue_recovery.py tests/test_glue_rpool.py \
+        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "not cluster_sim"
     timeout -k 10 200 "$A/glue_recovery_bench" 3
     timeout -k 10 200 "$A/glue_recovery_bench" set 16384 4098 2
     for s in 0 1 2; do timeout -k 10 200 "$A/glue_cluster_sim63" $s $s; done
@@ -64,9 +65,12 @@ glue)  # (here, on the CPU, where the reference's headers are) the glue programs
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -o "$A/glue_recovery" "$R/tests/glue/recovery_main.c" \
       "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" "$R/integration/cocytus_set.c" \
       -L"$A" -lcocytus_ec -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT
+  $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -o "$A/glue_rpool" "$R/tests/glue/rpool_main.c" \
+      "$R/integration/cocytus_recovery_pool.c" "$R/integration/cocytus_drain.c" \
+      -L"$A" -lcocytus_ec -Wl,-rpath,'$ORIGIN' -Wl,-rpath,$RT
   $CC $G -DK=6 -DM=3 -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_cluster_sim63" \
       "$R/tests/glue/cluster_sim.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" \
-      "$R/integration/cocytus_set.c" -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
+      "$R/integration/cocytus_set.c" "$R/integration/cocytus_recovery_pool.c" -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
       -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_recovery_bench" \
       "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_set.c" \
