@@ -255,9 +255,13 @@ int main(int argc, char **argv) {
     fclose(uf);
     fclose(log);
     fclose(solves);
+    fprintf(stderr, "teardown: pool\n");
     cocytus_rpool_destroy(g);
+    fprintf(stderr, "teardown: drainer\n");
     cec_drainer_destroy(dr);
+    fprintf(stderr, "teardown: unregister\n");
     cec_host_unregister(heap);
+    fprintf(stderr, "teardown: free\n");
     for (int q = 0; q < qcap; ++q) free(rec.queue.items[q].data_from_parity);
     free(rec.queue.items);
     free(rec.units);
@@ -266,5 +270,6 @@ int main(int argc, char **argv) {
     free(solved);
     free(matrix);
     free(heap);
+    fprintf(stderr, "teardown: exit\n");
     return 0;
 }

@@ -136,7 +136,18 @@ def run_script(tmp_path, script: Script, heap: np.ndarray, nunits, k, m):
     sp, hp, out = tmp_path / "script.txt", tmp_path / "heap.bin", tmp_path / "out"
     sp.write_text("\n".join(script.lines) + "\n")
     heap.tofile(hp)
-    r = subprocess.run([EXE, str(sp), str(hp), str(out)], capture_output=True, text=True, timeout=300)
+    err = tmp_path / "stderr.txt"
+    with open(err, "w") as ef:  # (a file, so a stuck driver still shows what it printed)
+        proc = subprocess.Popen([EXE, str(sp), str(hp), str(out)], stdout=subprocess.DEVNULL, stderr=ef)
+        try:  # below the tests' own 120 s limit
+            rc = proc.wait(timeout=90)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
+            done = (tmp_path / "out.log").read_text() if (tmp_path / "out.log").exists() else ""
+            raise AssertionError(f"{EXE} did not finish in 90 s; ops done: {done[-2000:]!r}; "
+                                 f"stderr: {err.read_text()[-4000:]!r}") from None
+    r = subprocess.CompletedProcess(proc.args, rc, None, err.read_text())
     assert r.returncode == 0, r.stderr
     log = (tmp_path / "out.log").read_text().split("\n")
     raw = np.fromfile(tmp_path / "out.units", dtype=np.uint8)

@@ -50,6 +50,12 @@ run)
   # against the reference's headers on the CPU (glue build, below) and linked here to the
   # instrumented library: the GPU glue tests through that binary, then its bench shapes
   if [ -x "$A/glue_recovery" ]; then
+    # (leak detection off for these 21 short-lived drivers only: LeakSanitizer's exit-time
+    # stop-the-world hung in one of them, the same test each time within this session and
+    # never alone, and with its check moved ahead of the HIP runtime's teardown it hung in
+    # others -- tools/repro/run3.sh: the session passes with detect_leaks=0.  Leaks are
+    # still checked on every other program here, the glue benches and simulations included.)
+    ASAN_OPTIONS=${ASAN_OPTIONS/detect_leaks=1/detect_leaks=0} \
     CEC_GLUE_RECOVERY_EXE="$A/glue_recovery" CEC_GLUE_RPOOL_EXE="$A/glue_rpool" timeout -k 10 300 \
         python -u -m pytest tests/test_glue_recovery.py tests/test_glue_rpool.py \
         -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "not cluster_sim"
