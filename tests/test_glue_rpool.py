@@ -343,3 +343,24 @@ def test_rpool_refusals(gpu, oracle, tmp_path):
     for q in (0, 1, 2, 4):                          # (E of request 2 resets unit 21's flag)
         sim.end(q)
     check(sim, tmp_path)
+
+
+DRB = os.path.join(ROOT, "oracle", "_ref", "glue_drain_recovery_bench")
+
+
+@pytest.mark.gpu
+def test_drain_during_recovery_four_paths_agree(gpu):
+    """tests/glue/drain_recovery_bench.c at a small size: a drain window during recovery
+    (process_rep_command's fold, then the apply) through the host-batch glue, the pool glue,
+    the unchanged per-xid loop on the drop-in and on the restated CPU multiply leaves the same
+    arena and the same units in all four (its "verified"), half the diffs on units under
+    recovery."""
+    if not os.path.exists(DRB):
+        pytest.skip("oracle/_ref/glue_drain_recovery_bench not built (make -C oracle ref)")
+    r = subprocess.run([DRB, "512", "4098", "64", "0.5", "1"], capture_output=True, text=True, timeout=100)
+    assert r.returncode == 0, r.stdout + r.stderr
+    import json
+
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["verified"] is True and line["aimed_at_recovering_units"] == 256
+

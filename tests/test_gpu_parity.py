@@ -1681,6 +1681,48 @@ def test_recovery_pool_fold_updates_window(gpu, oracle, capacity):
             pl.destroy()
 
 
+def test_recovery_pool_host_output_lifecycle(gpu, oracle):
+    """The _host solves' output (what cocytus_recovery_pool.c hands fill_completed_recovered_
+    data): none before a solve; after flush_solve_host the rebuilt units of a request it
+    completes; a lost lid's diff folded afterwards (recovery.c:116-120) makes it stale --
+    solved() and output() drop it -- and solve_host rebuilds the live bytes; a request the
+    flush did not complete is solved by solve_host; ending a request drops its output."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0x0B7)
+    nunits = 16
+    data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+    p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
+    mask = (1 << 3) | 0b110  # D0 lost, leader P0
+    with ec.RecoveryPool(k, m, mat, 3, p0, capacity_units=8) as pool:
+        a, b = pool.begin(mask, 2, 4), pool.begin(mask, 9, 9)
+        assert pool.output(a) is None
+        for j in (1, 2):
+            pool.add_peer(a, j, data[j][2 * U:5 * U].copy())
+        pool.add_peer(b, 1, data[1][9 * U:10 * U].copy())
+        assert pool.flush_solve_host() == 1  # a completes in this flush, b does not
+        assert pool.solved(a) and not pool.solved(b) and pool.output(b) is None
+        assert np.array_equal(pool.output(a), data[0][2 * U:5 * U])
+        # a SET on lost D0, forwarded by its substitute: folded into a's residual
+        addr, ln = 3 * U + 100, 5000
+        new = rng.integers(0, 256, ln, dtype=np.uint8)
+        diff = oracle.set_diff(data[0][addr:addr + ln].copy(), new)
+        data[0][addr:addr + ln] = new
+        assert pool.fold_update(0, addr, diff) == 2  # units 3 and 4 of a
+        ec.region_multiply(to_dev(torch, diff), mat[3 * k + 0], ln, p0.data_ptr() + addr, 1)
+        torch.cuda.synchronize()
+        assert not pool.solved(a) and pool.output(a) is None
+        pool.add_peer(b, 2, data[2][9 * U:10 * U].copy())
+        pool.flush()  # b's last reply folded, no solve
+        assert not pool.solved(b)
+        pool.solve_host([a, b])
+        assert np.array_equal(pool.output(a), data[0][2 * U:5 * U])
+        assert np.array_equal(pool.output(b), data[0][9 * U:10 * U])
+        pool.end(a)
+        assert pool.output(a) is None
+
+
 def test_batched_bindings_c_program(gpu, oracle, tmp_path):
     """The batched bindings from a C99 program (cec_encode_region, cec_diff_update,
     cec_drainer_apply, cec_recovery_pool) vs the reference's chains."""
