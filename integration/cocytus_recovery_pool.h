@@ -47,7 +47,8 @@ extern "C" {
 
 typedef struct cocytus_rpool cocytus_rpool;
 
-/* One per parity process.  parity_dev: this parity's arena as the device sees it (above);
+/* One per parity process, called from the thread that runs its recovery (like struct
+ * recovery itself, it takes no locks).  parity_dev: this parity's arena as the device sees it (above);
  * queue_cap: recovery.queue.cap (requests are keyed by their slot in recovery.queue.items);
  * capacity_units: residual slots (at least the largest request's units; the idle recoverer
  * needs 85).  stream: the worker thread's (NULL: the default stream). */

@@ -1632,14 +1632,17 @@ def test_recovery_pool_non_leader_residual_and_errors(gpu, oracle):
         assert pool.begin(0b11100, 10, 17) >= 0  # room again
 
 
+@pytest.mark.parametrize("engine_name", ["perm", "lds"])
 @pytest.mark.parametrize("capacity", [64, 12])
-def test_recovery_pool_fold_updates_window(gpu, oracle, capacity):
+def test_recovery_pool_fold_updates_window(gpu, oracle, capacity, engine_name):
     """A drain window folded at once (cec_recovery_pool_fold_updates) equals the same
     updates folded one by one (cec_recovery_pool_fold_update, recovery.c:99-131) on a twin
     pool: 300 SET diffs of every data lid -- lost ones too -- crowded onto few units, so
     they meet in R and split into waves; requests untouched, touched, complete and
     partly fed.  capacity 12: the window has more tiles than the pool's tile buffer."""
     torch, ec = gpu
+    default = ec.get_engine()
+    ec.set_engine(ec.CEC_ENGINE_PERM if engine_name == "perm" else ec.CEC_ENGINE_LDS)
     k, m, U = 4, 2, 4096
     mat = ec.coding_matrix(k, m)
     rng = np.random.default_rng(0xF01D + capacity)
@@ -1679,6 +1682,7 @@ def test_recovery_pool_fold_updates_window(gpu, oracle, capacity):
     finally:
         for pl in pools:
             pl.destroy()
+        ec.set_engine(default)
 
 
 def test_recovery_pool_host_output_lifecycle(gpu, oracle):
