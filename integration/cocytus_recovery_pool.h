@@ -48,8 +48,9 @@ extern "C" {
 typedef struct cocytus_rpool cocytus_rpool;
 
 /* One per parity process, called from the thread that runs its recovery (like struct
- * recovery itself, it takes no locks).  parity_dev: this parity's arena as the device sees it (above);
- * queue_cap: recovery.queue.cap (requests are keyed by their slot in recovery.queue.items);
+ * recovery itself, it takes no locks).  parity_dev: this parity's arena as the device sees
+ * it (above); queue_cap: recovery.queue.cap (requests are keyed by their slot in
+ * recovery.queue.items);
  * capacity_units: residual slots (at least the largest request's units; the idle recoverer
  * needs 85).  stream: the worker thread's (NULL: the default stream). */
 int cocytus_rpool_create(cocytus_rpool **out, int k, int m, const int *matrix, int self_lid, const void *parity_dev,
@@ -81,7 +82,8 @@ char *cocytus_rpool_staging(cocytus_rpool *g, struct recovery *r, const struct r
  * cocytus_rpool_end). */
 int cocytus_rpool_try_update_unit(cocytus_rpool *g, struct recovery *r, char *touch_flags, const char *sub_flags,
                                   int peerid, uint64_t addr, const char *data, uint32_t size);
-/* The same over a drain window (need[i] per update, in xid order). */
+/* The same over a drain window (need[i] per update, in xid order): every fold of the window
+ * in one cec_recovery_pool_fold_updates. */
 int cocytus_rpool_try_update_units(cocytus_rpool *g, struct recovery *r, char *const *touch_flags,
                                    const char *sub_flags, const cec_host_update *u, int n, int *need);
 
@@ -99,7 +101,9 @@ int cocytus_rpool_solve(cocytus_rpool *g, struct recovery *r, const struct recov
 int cocytus_rpool_flush(cocytus_rpool *g);
 /* After the flush that ran rqit's solve: data[x] of the bottom half (the x-th lost data lid,
  * units x UNITSIZE bytes), for fill_completed_recovered_data or the scatter send
- * (memcached.c:7935-7962).  Valid until cocytus_rpool_end; NULL before the solve ran. */
+ * (memcached.c:7935-7962).  Valid until cocytus_rpool_end; NULL before the solve ran, and
+ * for a single loss solved in the pool also once a later fold has changed its residual (a
+ * lost lid's SET: read the bytes right after the flush, as the bottom half does). */
 const char *cocytus_rpool_data(const cocytus_rpool *g, const struct recovery *r, const struct recovery_queue_item *rqit,
                                int x);
 /* Queued solves not yet run. */
