@@ -216,7 +216,10 @@ int main(int argc, char **argv) {
             int n = -1;
             const int rc = cocytus_rpool_solve(g, &rec, it, &n);
             fprintf(log, "S %d %d\n", rc, n);
-            if (rc == 0 && n > 0) solved[n_solved++] = qi;
+            if (rc == 0 && n > 0) {
+                if (n_solved == qcap * 4) return fprintf(stderr, "more than %d solves between flushes\n", qcap * 4), 2;
+                solved[n_solved++] = qi;
+            }
         } else if (!strcmp(op, "F")) {
             const int rc = cocytus_rpool_flush(g);
             fprintf(log, "F %d\n", rc);
