@@ -50,18 +50,22 @@ run)
   # against the reference's headers on the CPU (glue build, below) and linked here to the
   # instrumented library: the GPU glue tests through that binary, then its bench shapes
   if [ -x "$A/glue_recovery" ]; then
-    # (leak detection off for these 21 short-lived drivers only: LeakSanitizer's exit-time
-    # stop-the-world hung in one of them, the same test each time within this session and
-    # never alone, and with its check moved ahead of the HIP runtime's teardown it hung in
-    # others -- tools/repro/run3.sh: the session passes with detect_leaks=0.  Leaks are
-    # still checked on every other program here, the glue benches and simulations included.)
-    ASAN_OPTIONS=${ASAN_OPTIONS/detect_leaks=1/detect_leaks=0} \
+    # test_rpool_refusals's driver, alone, with LeakSanitizer off: at its exit LSan's
+    # stop-the-world attached to the main thread and two HIP runtime threads and then waited
+    # forever on the next one (LSAN_OPTIONS=verbosity=2, tools/repro/run4.sh,
+    # profiles/r05_evidence/lsan_hang/) -- whenever other GPU processes had run on the box
+    # before it, in one pytest session or in separate ones.  Its refusals allocate nothing
+    # (every check comes before any allocation); the other 20 run with leak detection on.
     CEC_GLUE_RECOVERY_EXE="$A/glue_recovery" CEC_GLUE_RPOOL_EXE="$A/glue_rpool" timeout -k 10 300 \
         python -u -m pytest tests/test_glue_recovery.py tests/test_glue_rpool.py \
-        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "not cluster_sim"
+        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -k "not cluster_sim and not refusals"
+    ASAN_OPTIONS=${ASAN_OPTIONS/detect_leaks=1/detect_leaks=0} CEC_GLUE_RPOOL_EXE="$A/glue_rpool" \
+        timeout -k 10 200 python -u -m pytest tests/test_glue_rpool.py \
+        -m gpu -v --timeout 120 --timeout-method thread -p no:cacheprovider -k refusals
     timeout -k 10 200 "$A/glue_recovery_bench" 3
     timeout -k 10 200 "$A/glue_recovery_bench" set 16384 4098 2
     for s in 0 1 2; do timeout -k 10 200 "$A/glue_cluster_sim63" $s $s; done
+    timeout -k 10 200 "$A/glue_drain_recovery_bench" 1024 4098 64 0.5 1
   fi
   ;;
 glue)  # (here, on the CPU, where the reference's headers are) the glue programs against tools/asan
@@ -77,6 +81,10 @@ glue)  # (here, on the CPU, where the reference's headers are) the glue programs
   $CC $G -DK=6 -DM=3 -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_cluster_sim63" \
       "$R/tests/glue/cluster_sim.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_drain.c" \
       "$R/integration/cocytus_set.c" "$R/integration/cocytus_recovery_pool.c" -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
+      -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
+  $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_drain_recovery_bench" \
+      "$R/tests/glue/drain_recovery_bench.c" "$R/integration/cocytus_drain.c" "$R/integration/cocytus_recovery.c" \
+      "$R/integration/cocytus_recovery_pool.c" -L"$A" -lcocytus_ec -L"$R/oracle" -lgf8ref -Wl,-rpath,'$ORIGIN' \
       -Wl,-rpath,'$ORIGIN/../../oracle' -Wl,-rpath,$RT
   $CC $G -I"$R/include" -I"$R/integration" -I"$REF" -I"$R/oracle" -o "$A/glue_recovery_bench" \
       "$R/tests/glue/recovery_bench.c" "$R/integration/cocytus_recovery.c" "$R/integration/cocytus_set.c" \
