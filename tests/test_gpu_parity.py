@@ -1727,6 +1727,42 @@ def test_recovery_pool_host_output_lifecycle(gpu, oracle):
         assert pool.output(a) is None
 
 
+def test_recovery_pool_misuse_is_refused(gpu, oracle):
+    """Stale and bad handles on the pool's calls (what a server bug would send): an ended or
+    never-begun id, a repeated end, a reply or a solve for an ended request, a window with a
+    data lid out of range -- each refused (CecError / None), nothing crashes, and a live
+    request next to them still rebuilds its bytes."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xBAD)
+    data = [rng.integers(0, 256, 8 * U, dtype=np.uint8) for _ in range(k)]
+    p0 = to_dev(torch, oracle.encode(mat, k, m, data)[0])
+    mask = (1 << 3) | 0b110
+    with ec.RecoveryPool(k, m, mat, 3, p0, capacity_units=4) as pool:
+        dead, live = pool.begin(mask, 0, 0), pool.begin(mask, 5, 5)
+        pool.end(dead)
+        for bad in (dead, 7, -1, 1 << 20):
+            with pytest.raises(ec.CecError):
+                pool.end(bad)
+            with pytest.raises(ec.CecError):
+                pool.add_peer(bad, 1, data[1][:U].copy())
+            with pytest.raises(ec.CecError):
+                pool.solve_host([bad])
+            assert pool.output(bad) is None and not pool.solved(bad) and not pool.complete(bad)
+        with pytest.raises(ec.CecError):
+            pool.fold_updates([(np.zeros(16, np.uint8), 0, k)])  # data lid k: out of range
+        with pytest.raises(ec.CecError):
+            pool.add_peer(live, 3, data[1][5 * U:6 * U].copy())  # a parity lid is no data peer
+        for j in (1, 2):
+            pool.add_peer(live, j, data[j][5 * U:6 * U].copy())
+        with pytest.raises(ec.CecError):
+            pool.solve_host([live, live])  # listed twice
+        pool.solve_host([live])
+        assert np.array_equal(pool.output(live), data[0][5 * U:6 * U])
+        assert pool.active == 1
+
+
 def test_batched_bindings_c_program(gpu, oracle, tmp_path):
     """The batched bindings from a C99 program (cec_encode_region, cec_diff_update,
     cec_drainer_apply, cec_recovery_pool) vs the reference's chains."""
