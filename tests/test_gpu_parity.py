@@ -569,6 +569,56 @@ def test_drainer_matches_sequential_loop(gpu, oracle, engine, staging):
     assert np.array_equal(to_host(dev), parity)
 
 
+@pytest.mark.parametrize("arena_kind", ["device", "registered_host"])
+def test_drainer_small_windows(gpu, oracle, arena_kind):
+    """Windows of 1 to ~60 diffs -- the small-window path (one pass of the caller's thread
+    into mapped staging, no pack threads or uploads) and, at the edges, the pack path: each
+    window, overlapping and ragged updates included, leaves the arena as the reference's
+    drain loop (memcached.c:7762-7767), in HBM and in a registered host arena (its results
+    fenced for the host on return: read without a device sync)."""
+    torch, ec = gpu
+    k, m = 3, 2
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0x5A11 + len(arena_kind))
+    arena = 1 << 20
+    parity = rng.integers(0, 256, arena, dtype=np.uint8)
+    host = None
+    if arena_kind == "device":
+        dev = to_dev(torch, parity)
+    else:
+        host = parity.copy()
+        dev = ec.host_register(host)
+    lid_self = k
+    try:
+        with ec.Drainer(k, m, mat, lid_self, staging_bytes=1 << 20) as d:
+            for n_ups, max_len in ((1, 16), (1, 4098), (5, 9000), (40, 3000), (60, 4400), (80, 4098),
+                                   (200, 8000), (300, 8000)):
+                ups = []
+                for i in range(n_ups):
+                    ln = int(rng.integers(1, max_len + 1))
+                    if i % 7 == 3 and ups:  # on top of an earlier one: a second wave
+                        addr = min(ups[-1][1] + 16, arena - ln)
+                    else:
+                        addr = int(rng.integers(0, (arena - ln) // 16)) * 16 + (5 if i % 11 == 10 else 0)
+                    ups.append((rng.integers(0, 256, ln, dtype=np.uint8), addr, int(rng.integers(0, k))))
+                small = sum((b.size + 15) // 16 * 16 for b, _, _ in ups) <= 1 << 20
+                d.apply(ups, dev)
+                for buf, addr, j in ups:
+                    v = parity[addr:addr + buf.size].copy()
+                    oracle.parity_apply(mat, k, lid_self, j, buf, v)
+                    parity[addr:addr + buf.size] = v
+                if host is not None:  # on return, no device sync
+                    assert np.array_equal(host, parity), (n_ups, max_len)
+                    if small:  # the small-window path's completion: fenced for the host
+                        sync = ec.last_sync()
+                        assert (sync["host_results"], sync["fenced"]) == (1, 1)
+                else:
+                    assert np.array_equal(to_host(dev), parity), (n_ups, max_len)
+    finally:
+        if host is not None:
+            ec.host_unregister(host)
+
+
 def test_drainer_full_size(gpu, oracle):
     """The batched drain at the bench's size: 65,536 pending 4 KiB
     diffs in pageable host memory, source shard uniform in {0,1,2}, addresses shuffled
