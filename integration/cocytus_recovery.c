@@ -182,11 +182,19 @@ int cocytus_recover_units_defer(cocytus_rglue *g, struct recovery *r, struct ecm
     return CEC_OK;
 }
 
-/* recovery_try_update_unit's walk (recovery.c:105-129) over one update, folds appended */
-static int try_update_walk(cocytus_rglue *g, struct recovery *r, char *touch_flags, const char *sub_flags,
-                           int peerid, uint64_t addr, const char *data, uint32_t size, cec_region_job **jobs,
-                           int *n, int *cap) {
-    int ret = 0;
+/* recovery_try_update_unit's walk (recovery.c:105-129) over one update, in two passes so that
+ * a refusal changes nothing (cocytus_recovery.h: the reference's checks come first):
+ *   check  (commit == 0): no write; CEC_EINVAL if a piece would fold into a unit with UPDATE
+ *          set and no data (the reference would dereference NULL at recovery.c:123), else the
+ *          number of folds the update makes;
+ *   commit (commit != 0): touch_flags set, folds appended at (*jobs)[*n] (the caller grew
+ *          the array by the check's count), returns what the reference returns.
+ * struct recovery carries no unit count: the unit index is bounded by the server's arena, as
+ * in recovery_get_unit. */
+static int try_update_walk(const cocytus_rglue *g, struct recovery *r, char *touch_flags, const char *sub_flags,
+                           int peerid, uint64_t addr, const char *data, uint32_t size, int commit,
+                           cec_region_job *jobs, int *n) {
+    int ret = 0, folds = 0;
     const int c = MAT(g, g->self, peerid);
     while (size > 0) {
         const uint64_t offset = addr % UNIT;
@@ -194,33 +202,72 @@ static int try_update_walk(cocytus_rglue *g, struct recovery *r, char *touch_fla
         uint32_t len = (uint32_t)(UNIT - offset);
         if (size < len) len = size;
         size -= len;
-        if (touch_flags) touch_flags[base / UNIT] = 1;                    /* :112 */
+        if (commit && touch_flags) touch_flags[base / UNIT] = 1;           /* :112 */
         if (sub_flags == NULL || sub_flags[base / UNIT] != 2) ret++;      /* :113 */
         struct recovery_unit *u = &r->units[base / UNIT];
         /* :116-120: recovered, not taking updates, or this peer's bytes already in */
         if (!(u->flags & F_RECOVERED) && (u->flags & F_UPDATE) && !(u->flags & F_LID(peerid))) {
             if (!u->data) return CEC_EINVAL;
-            int rc = grow((void **)jobs, cap, *n + 1, sizeof **jobs);
-            if (rc) return rc;
-            cec_region_job *j = &(*jobs)[(*n)++];
-            j->src = data;
-            j->dst = u->data + offset;
-            j->base = NULL;
-            j->len = len;
-            j->multby = c;
-            j->add = 1;
+            folds++;
+            if (commit) {
+                cec_region_job *j = &jobs[(*n)++];
+                j->src = data;
+                j->dst = u->data + offset;
+                j->base = NULL;
+                j->len = len;
+                j->multby = c;
+                j->add = 1;
+            }
         }
         addr += len;
         data += len;
     }
-    return ret;
+    return commit ? ret : folds;
+}
+
+/* Both passes over a window of updates (a single update is a window of one): every update
+ * checked, then *jobs grown by the folds of all of them, then committed -- a refused window
+ * leaves touch_flags, need[] and the queue as they were.  *src_bytes (optional) receives
+ * the bytes the folds read. */
+static int try_update_window(cocytus_rglue *g, struct recovery *r, char *const *touch_flags, char *touch_one,
+                             const char *sub_flags, const cec_host_update *u, int n, int *need,
+                             cec_region_job **jobs, int *nj, int *cap) {
+    int folds = 0;
+    for (int i = 0; i < n; ++i) {
+        const int lid = (int)u[i].src_lid;
+        const int f = try_update_walk(g, r, NULL, sub_flags, lid, u[i].addr, (const char *)u[i].buf, u[i].len, 0,
+                                      NULL, NULL);
+        if (f < 0) return f;
+        folds += f;
+    }
+    int rc = grow((void **)jobs, cap, *nj + folds, sizeof **jobs);
+    if (rc) return rc;
+    int last = 0;
+    for (int i = 0; i < n; ++i) {
+        const int lid = (int)u[i].src_lid;
+        char *tf = touch_flags ? touch_flags[lid] : touch_one;
+        last = try_update_walk(g, r, tf, sub_flags, lid, u[i].addr, (const char *)u[i].buf, u[i].len, 1, *jobs, nj);
+        if (need) need[i] = last;
+    }
+    return last;
+}
+
+/* one update as a window of one */
+static cec_host_update one_update(int peerid, uint64_t addr, const char *data, uint32_t size) {
+    cec_host_update x;
+    x.buf = data;
+    x.addr = addr;
+    x.len = size;
+    x.src_lid = (uint32_t)peerid;
+    return x;
 }
 
 int cocytus_try_update_unit_gf(cocytus_rglue *g, struct recovery *r, char *touch_flags, const char *sub_flags,
                                int peerid, uint64_t addr, const char *data, uint32_t size) {
     if (!g || !r || !r->units || peerid < 0 || peerid >= g->k || (size && !data)) return CEC_EINVAL;
+    const cec_host_update x = one_update(peerid, addr, data, size);
     int n = 0;
-    const int ret = try_update_walk(g, r, touch_flags, sub_flags, peerid, addr, data, size, &g->tmp, &n, &g->cap_tmp);
+    const int ret = try_update_window(g, r, NULL, touch_flags, sub_flags, &x, 1, NULL, &g->tmp, &n, &g->cap_tmp);
     if (ret < 0) return ret;
     if (n) {
         const int rc = cec_region_multiply_batch(g->tmp, n, g->stream);
@@ -229,32 +276,37 @@ int cocytus_try_update_unit_gf(cocytus_rglue *g, struct recovery *r, char *touch
     return ret;
 }
 
-int cocytus_try_update_units_gf(cocytus_rglue *g, struct recovery *r, char *const *touch_flags,
-                                const char *sub_flags, const cec_host_update *u, int n, int *need) {
+static int check_window(const cocytus_rglue *g, const struct recovery *r, const cec_host_update *u, int n, int *need) {
     if (!g || !r || !r->units || n < 0 || (n && (!u || !need))) return CEC_EINVAL;
     for (int i = 0; i < n; ++i)
         if (u[i].src_lid >= (uint32_t)g->k || (u[i].len && !u[i].buf)) return CEC_EINVAL;
+    return CEC_OK;
+}
+
+int cocytus_try_update_units_gf(cocytus_rglue *g, struct recovery *r, char *const *touch_flags,
+                                const char *sub_flags, const cec_host_update *u, int n, int *need) {
+    int rc = check_window(g, r, u, n, need);
+    if (rc) return rc;
     int nj = 0;
-    for (int i = 0; i < n; ++i) {
-        const int lid = (int)u[i].src_lid;
-        const int ret = try_update_walk(g, r, touch_flags ? touch_flags[lid] : NULL, sub_flags, lid, u[i].addr,
-                                        (const char *)u[i].buf, u[i].len, &g->tmp, &nj, &g->cap_tmp);
-        if (ret < 0) return ret;
-        need[i] = ret;
-    }
+    rc = try_update_window(g, r, touch_flags, NULL, sub_flags, u, n, need, &g->tmp, &nj, &g->cap_tmp);
+    if (rc < 0) return rc;
     return nj ? cec_region_multiply_batch(g->tmp, nj, g->stream) : CEC_OK;
 }
 
 /* Deferred folds outlive the diffs they read (rep_queue_flush frees e->vbuf once the xid
- * is processed, rep_queue.c:86-103): copy the pieces of folds [from, n_fold) into one
- * buffer the glue owns until the flush. */
-static int own_sources(cocytus_rglue *g, int from) {
-    if (from == g->n_fold) return CEC_OK;
-    size_t total = 0;
-    for (int i = from; i < g->n_fold; ++i) total += g->fold[i].len;
+ * is processed, rep_queue.c:86-103): the pieces of folds [from, n_fold) are copied into
+ * one buffer the glue owns until the flush.  Reserved before the commit (so an ENOMEM
+ * changes nothing), filled after it. */
+static int own_reserve(cocytus_rglue *g, size_t total, char **buf) {
+    *buf = NULL;
+    if (total == 0) return CEC_OK;
     if (grow((void **)&g->owned, &g->cap_owned, g->n_owned + 1, sizeof *g->owned)) return CEC_ENOMEM;
-    char *buf = malloc(total);
-    if (!buf) return CEC_ENOMEM;
+    *buf = malloc(total);
+    return *buf ? CEC_OK : CEC_ENOMEM;
+}
+
+static void own_fill(cocytus_rglue *g, int from, char *buf) {
+    if (!buf) return;
     size_t o = 0;
     for (int i = from; i < g->n_fold; ++i) {
         memcpy(buf + o, g->fold[i].src, g->fold[i].len);
@@ -262,45 +314,58 @@ static int own_sources(cocytus_rglue *g, int from) {
         o += g->fold[i].len;
     }
     g->owned[g->n_owned++] = buf;
+}
+
+/* the bytes the folds of a window read (an upper bound: every piece of a folding unit) */
+static int window_fold_bytes(const cocytus_rglue *g, struct recovery *r, const char *sub_flags,
+                             const cec_host_update *u, int n, size_t *total) {
+    *total = 0;
+    for (int i = 0; i < n; ++i) {
+        const int f = try_update_walk(g, r, NULL, sub_flags, (int)u[i].src_lid, u[i].addr, (const char *)u[i].buf,
+                                      u[i].len, 0, NULL, NULL);
+        if (f < 0) return f;
+        if (f) *total += u[i].len;
+    }
     return CEC_OK;
+}
+
+static int try_update_defer(cocytus_rglue *g, struct recovery *r, char *const *touch_flags, char *touch_one,
+                            const char *sub_flags, const cec_host_update *u, int n, int *need) {
+    size_t total;
+    int rc = window_fold_bytes(g, r, sub_flags, u, n, &total);
+    if (rc) return rc;
+    char *buf;
+    if ((rc = own_reserve(g, total, &buf))) return rc;
+    const int before = g->n_fold;
+    const int ret = try_update_window(g, r, touch_flags, touch_one, sub_flags, u, n, need, &g->fold, &g->n_fold,
+                                      &g->cap_fold);
+    if (ret < 0) { /* (the window's checks ran in window_fold_bytes: only grow's ENOMEM) */
+        g->n_fold = before;
+        free(buf);
+        return ret;
+    }
+    if (g->n_fold > before) {
+        own_fill(g, before, buf);
+        g->req_fold++;
+    } else {
+        free(buf);
+    }
+    return ret;
 }
 
 int cocytus_try_update_units_defer(cocytus_rglue *g, struct recovery *r, char *const *touch_flags,
                                    const char *sub_flags, const cec_host_update *u, int n, int *need) {
-    if (!g || !r || !r->units || n < 0 || (n && (!u || !need))) return CEC_EINVAL;
-    for (int i = 0; i < n; ++i)
-        if (u[i].src_lid >= (uint32_t)g->k || (u[i].len && !u[i].buf)) return CEC_EINVAL;
-    const int before = g->n_fold;
-    for (int i = 0; i < n; ++i) {
-        const int lid = (int)u[i].src_lid;
-        const int ret = try_update_walk(g, r, touch_flags ? touch_flags[lid] : NULL, sub_flags, lid, u[i].addr,
-                                        (const char *)u[i].buf, u[i].len, &g->fold, &g->n_fold, &g->cap_fold);
-        if (ret < 0) {
-            g->n_fold = before; /* nothing of this call stays queued */
-            return ret;
-        }
-        need[i] = ret;
-    }
-    if (own_sources(g, before)) {
-        g->n_fold = before;
-        return CEC_ENOMEM;
-    }
-    if (g->n_fold > before) g->req_fold++;
-    return CEC_OK;
+    int rc = check_window(g, r, u, n, need);
+    if (rc) return rc;
+    rc = try_update_defer(g, r, touch_flags, NULL, sub_flags, u, n, need);
+    return rc < 0 ? rc : CEC_OK;
 }
 
 int cocytus_try_update_unit_defer(cocytus_rglue *g, struct recovery *r, char *touch_flags, const char *sub_flags,
                                   int peerid, uint64_t addr, const char *data, uint32_t size) {
     if (!g || !r || !r->units || peerid < 0 || peerid >= g->k || (size && !data)) return CEC_EINVAL;
-    const int before = g->n_fold;
-    const int ret = try_update_walk(g, r, touch_flags, sub_flags, peerid, addr, data, size, &g->fold, &g->n_fold,
-                                    &g->cap_fold);
-    if (ret < 0 || own_sources(g, before)) {
-        g->n_fold = before;
-        return ret < 0 ? ret : CEC_ENOMEM;
-    }
-    if (g->n_fold > before) g->req_fold++;
-    return ret;
+    const cec_host_update x = one_update(peerid, addr, data, size);
+    return try_update_defer(g, r, NULL, touch_flags, sub_flags, &x, 1, NULL);
 }
 
 int cocytus_fold_hook(const cec_host_update *u, int n, int *need, void *ctx) {

@@ -261,6 +261,37 @@ def test_defer_refuses_what_the_reference_asserts(oracle, tmp_path):
     assert jobs_from_log(log) == mod.queue
 
 
+def test_try_update_refusal_changes_nothing(oracle, tmp_path):
+    """A unit with UPDATE set and no data (the reference would dereference NULL at
+    recovery.c:123): a try-update that would fold into it is refused (CEC_EINVAL) before
+    anything changes -- in a window, even when the offending update is the third, the
+    earlier updates' touch_flags, need[] and the fold queue stay as they were; the same for
+    the single-update calls, deferred and immediate (refused before any GPU pass)."""
+    _need_exe()
+    k, m, s, n = 3, 2, 4, 32
+    rng, heap, mod, sc = _setup(oracle, k, m, s, n, seed=5)
+    base = n * U
+    sc.add("D", 0, 0, 7, base)                   # units 0..7 touched (first touch, D0 in)
+    mod.recover(0, 0, 7, base, defer=True)
+    sc.add("flag", 20, F_UPDATE, -1)             # UPDATE without data
+    mod.flags[20] = F_UPDATE
+    window = [(1, 1 * U + 64, 300, base + 9 * U), (2, 3 * U, 2 * U, base + 10 * U),
+              (1, 19 * U + 4000, 200, base + 12 * U), (2, 5 * U, 100, base + 13 * U)]
+    for op in ("w", "W"):
+        sc.add(op, len(window))
+        for w in window:
+            sc.add(*w)
+    sc.add("t", 2, 20 * U + 8, 64, base + 14 * U)
+    sc.add("T", 1, 19 * U + 4090, 20, base + 14 * U)
+    sc.add("P")
+    log, flags, data, touch, _, _ = run_script(tmp_path, sc, heap, n, k, m)
+    lines = [ln.split() for ln in log]
+    assert [ln for ln in lines if ln[0] in "wW"] == [["w", "-1", "0", "0", "0", "0"], ["W", "-1", "0", "0", "0", "0"]]
+    assert [ln for ln in lines if ln[0] in "tT"] == [["t", "-1"], ["T", "-1"]]
+    check_state(mod, flags, data, touch)         # no touch_flags byte written by the refusals
+    assert jobs_from_log(log) == mod.queue       # only the reply's folds queued
+
+
 def _random_script(oracle, seed, k, m, s, n, gpu_ops=False):
     """Random ranges / diffs / flags: replies of every data peer (each unit at most once
     per peer, as the protocol delivers), SET diffs of any lid at any address and size,
