@@ -65,7 +65,20 @@ EXTRA_WORKLOADS = {
     "rs32_1m_recovery": "BASELINE configs[4] as stated: online recovery decode of ONE lost data shard "
                         "(every stripe the same), 1,024 x 1 MiB values, device-resident; D0 led by P0 "
                         "(inverse 1) and D1 led by P1 (inverse 1/245), SURVEY §8d",
+    # The server placements: the state where the
+    # unchanged server keeps it -- host memory, the arena registered once -- through the
+    # library API only, each beside the reference's 1-thread CPU loop (restated).
+    "drain_host_ecmem": "parity drain (memcached.c:4350 -> 7739-7767): 65,536 pageable 4098-B diffs at "
+                        "shuffled slots of a host ecmem registered with cec_host_register, one "
+                        "cec_drainer_apply per step",
+    "recovery_pool_host": "recovery into a cec_recovery_pool over a registered host ecmem "
+                          "(recovery.c:61-96 + memcached.c:7842-7922; idle recoverer memcached.c:5712-5734): "
+                          "one 1 MiB range and an 85-request idle pass, replies received into the pool's "
+                          "staging, ONE add_peers + flush_solve_host per pass, rebuilt bytes read in place",
+    "set_diffs_host": "data-side SET diffs (memcached.c:2676-2681): 65,536 SETs of 4098 B, pageable values, "
+                      "shuffled addresses of a registered host ecmem, one cec_region_multiply_batch per step",
 }
+SERVER_WORKLOADS = ("drain_host_ecmem", "recovery_pool_host", "set_diffs_host")
 
 
 def parse(argv=None):
@@ -94,7 +107,8 @@ def parse(argv=None):
                     help="run only the multi-rank harness (gloo, no GPU): launcher, shards, "
                          "barriers, max over ranks")
     ap.add_argument("--also", default="rs32_4k_lds,rs32_mixed,rs32_1m,rs42_64k,rs32_1m_recovery,"
-                                      "rs32_diff_update,rs32_diff_update_lds,rs32_e2e",
+                                      "rs32_diff_update,rs32_diff_update_lds,rs32_e2e,"
+                                      "drain_host_ecmem,recovery_pool_host,set_diffs_host",
                     help="other workloads measured after the main one, reported under "
                          "other_workloads ('' = none)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -870,6 +884,249 @@ def measure_e2e(torch, dist, ec, world, rank, args):
     return out
 
 
+def host_array(nbytes: int, fill_seed=None):
+    """A page-aligned uint8 numpy array of nbytes in ordinary (pageable) host memory, filled
+    with seeded random bytes when fill_seed is given (the server's malloc / mmap memory)."""
+    import numpy as np
+
+    raw = np.empty(nbytes + 4096, np.uint8)
+    off = (-raw.ctypes.data) % 4096
+    a = raw[off:off + nbytes]
+    if fill_seed is not None:
+        rng = np.random.default_rng(fill_seed)
+        step = 64 << 20
+        for o in range(0, nbytes, step):
+            n = min(step, nbytes - o)
+            a[o:o + n] = np.frombuffer(rng.bytes(n), np.uint8)
+    return a
+
+
+def _cpu_entry(gib, ts, sample):
+    """cpu_baseline block of a server-placement entry: the 1-thread restated loop, median of
+    the timed passes."""
+    t = statistics.median(ts)
+    return {"value": round(gib / t, 3), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "label": "restated CPU baseline", "median_ms": round(t * 1e3, 3),
+            "samples_ms": [round(x * 1e3, 3) for x in ts], "host": host_cpu(), "sample": sample}
+
+
+def measure_drain_host(torch, dist, ec, world, rank, args):
+    """SURVEY §8f rank 1, as the unchanged server would run it: the
+    parity P1 drains 65,536 pending 4098-B diffs -- each in pageable host memory at its own
+    shuffled slot, as malloc'd e->vbuf are -- into its host ecmem at shuffled 16-B aligned
+    addresses, the arena registered once (cec_host_register).  One cec_drainer_apply per
+    step (synchronous).  CPU beside it: the reference's loop, one region multiply per diff,
+    one thread (memcached.c:4350 -> process_rep_command :7764), the restated GF-Complete
+    kernel -- and its result is the check: after the timed steps the arena has taken the
+    window an odd number of times, so it must equal one oracle application."""
+    import numpy as np
+    from oracle import pyoracle
+
+    k, m, N, size = 3, 2, 65536, 4098
+    stride = (size + 15) & ~15
+    lid_self = k + 1
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xC0C70007 + rank)
+    arena = host_array(N * stride, 0xC0C70008 + rank)
+    initial = arena.copy()
+    diffs = host_array(N * stride, 0xC0C70009 + rank)
+    dslot = rng.permutation(N).astype(np.uint64)
+    addrs = rng.permutation(N).astype(np.uint64) * np.uint64(stride)
+    src = rng.integers(0, k, N)
+    base = diffs.ctypes.data
+    upd = ec.host_updates([(base + int(dslot[i]) * stride, int(addrs[i]), int(src[i]), size) for i in range(N)])
+    stream = torch.cuda.current_stream()
+    alias = ec.host_register(arena)
+    try:
+        with ec.Drainer(k, m, mat, lid_self, staging_bytes=64 << 20) as d:
+            warm = max(1, args.warmup)
+            for _ in range(warm):
+                d.apply(upd, alias, stream)
+            if dist_on(dist):
+                dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                launches = d.apply(upd, alias, stream)  # synchronous: applied on return
+            el = time.perf_counter() - t0
+            if dist_on(dist):
+                dist.barrier()
+            applied = warm + args.steps
+            if applied % 2 == 0:  # (an odd count: the arena holds ONE application)
+                d.apply(upd, alias, stream)
+    finally:
+        ec.host_unregister(arena)
+    cpu = initial
+    coefs = [mat[lid_self * k + int(j)] for j in src]
+    lens = np.full(N, size, np.uint32)
+    ts = [pyoracle.bench_apply(diffs, dslot * np.uint64(stride), addrs, lens, coefs, cpu) for _ in range(3)]
+    ok = bool(np.array_equal(arena, cpu))  # 3 oracle passes: one application as well
+    own = el
+    el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
+    gib = N * size / 2**30
+    out = {"value": round(gib * world * args.steps / el, 2), "unit": "GiB/s of diffs",
+           "ms_per_step": round(el * 1e3 / args.steps, 3), "us_per_diff": round(el * 1e6 / args.steps / N, 4),
+           "workload": EXTRA_WORKLOADS["drain_host_ecmem"], "launches_per_apply": launches,
+           "verified": ok and bad == 0.0,
+           "rank": {"ms_per_step": round(own * 1e3 / args.steps, 3), "verified": ok}}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_entry(gib, ts, "the reference's drain loop over the same 65,536 diffs "
+                                                  "(pageable, same slots and addresses), one region multiply "
+                                                  "per diff, 1 thread, median of 3 passes")
+        out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+    return out
+
+
+def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
+    """SURVEY §8f rank 2 in the pool placement: RS(3,2), this parity
+    P1 leads the recovery of lost D1 (mask D0 + D2 + P1, start_recovery's), its ecmem in
+    host memory registered once.  Two passes: one 1 MiB range (256 units) and the idle
+    recoverer's 85 single-unit requests in flight (const.h:27).  Per pass: the requests
+    begun and both data peers' replies received into the pool's staging (the recv, untimed
+    as every path's recv into c->vbuf), then -- timed -- ONE cec_recovery_pool_add_peers
+    and ONE cec_recovery_pool_flush_solve_host (fold + first-touch copy + leader solve in
+    one launch), after which the rebuilt bytes are read in place.  Every rep recovers other
+    units, 32 MiB further into a host arena, so the parity units are read cold.  CPU
+    beside it: the reference's per-unit chain (malloc'd units, recovery.c:72-94, then the
+    bottom half) on one thread over the same units and replies; its outputs check every
+    rep's rebuilt bytes."""
+    import numpy as np
+    from oracle import pyoracle
+
+    k, m, U, SELF, lost, peers = 3, 2, 4096, 4, 1, (0, 2)
+    mat = ec.coding_matrix(k, m)
+    mask = ec.recovery_mask(k, m, SELF, [int(i != lost) for i in range(k + m)])
+    inv = ec.galois_single_divide(1, mat[SELF * k + lost])
+    coefs = [mat[SELF * k + p] for p in peers]
+    reps = max(3, min(args.steps, 15))
+    walk = 8192  # units (32 MiB) between consecutive reps' ranges
+    nunits = walk * (reps + 2)
+    ecmem = host_array(nunits * U, 0xC0C7000A + rank)
+    rng = np.random.default_rng(0xC0C7000B + rank)
+    starts85 = (512 + rng.choice(walk - 512, 85, replace=False)).tolist()
+    alias = ec.host_register(ecmem)
+    shapes, ok = {}, True
+    try:
+        for name, units, starts in (("range_1MiB", 256, [100]), ("idle_85", 1, starts85)):
+            nreq = len(starts)
+            replies = [host_array(units * U, 0xC0C70100 + 7 * rank + x) for x in range(2 * nreq)]
+            gpu_t, cpu_t = [], []
+            with ec.RecoveryPool(k, m, mat, SELF, alias, capacity_units=nreq * units) as pool:
+                for rep in range(reps + 1):  # rep 0: warm-up
+                    first = [s + rep * walk for s in starts]
+                    rids = [pool.begin(mask, u0, u0 + units - 1) for u0 in first]
+                    ids, lids, stg = [], [], []
+                    for q, rid in enumerate(rids):
+                        for p, peer in enumerate(peers):
+                            addr, view = pool.staging(rid, peer)
+                            view[:] = replies[2 * q + p]  # the recv into c->ritem (untimed)
+                            ids.append(rid)
+                            lids.append(peer)
+                            stg.append(addr)
+                    arrs = ec.pool_replies(ids, lids, stg)
+                    if dist_on(dist):
+                        dist.barrier()
+                    t0 = time.perf_counter()
+                    pool.add_peers(arrs)
+                    solved = pool.flush_solve_host()
+                    t1 = time.perf_counter()
+                    got = [pool.output(rid).copy() for rid in rids]  # fill_completed_recovered_data
+                    for rid in rids:
+                        pool.end(rid)
+                    tc, exp = pyoracle.bench_recover_requests(ecmem, first, units, replies, 2, coefs, inv)
+                    ok &= solved == nreq and all(np.array_equal(g, e) for g, e in zip(got, exp))
+                    if rep:
+                        gpu_t.append(t1 - t0)
+                        cpu_t.append(tc)
+            g_med, c_med = statistics.median(gpu_t), statistics.median(cpu_t)
+            g_max = max_over_ranks([g_med], dist)[0]
+            gib = 3 * nreq * units * U / 2**30  # two replies folded + the bytes rebuilt
+            shapes[name] = {"requests": nreq, "units_per_request": units, "reps": reps,
+                            "us": round(g_max * 1e6, 1), "value": round(gib * world / g_max, 3),
+                            "unit": "GiB/s (replies folded + bytes rebuilt)",
+                            "rank_us": round(g_med * 1e6, 1)}
+            if world == 1 and not args.no_cpu_baseline:
+                shapes[name]["cpu_baseline"] = _cpu_entry(
+                    gib, cpu_t, f"the reference's chain for the same {nreq} request(s) x {units} unit(s): "
+                                "per reply and unit malloc + parity copy + region multiply, then the bottom "
+                                "half, 1 thread, cold parity units, median of the reps")
+                shapes[name]["cpu_us"] = round(c_med * 1e6, 1)
+                shapes[name]["gpu_over_cpu"] = round(c_med / g_max, 2)
+    finally:
+        ec.host_unregister(ecmem)
+    ok, = [x == 0.0 for x in max_over_ranks([0.0 if ok else 1.0], dist)]
+    out = {"value": shapes["range_1MiB"]["value"], "unit": shapes["range_1MiB"]["unit"] + ", 1 MiB range",
+           "workload": EXTRA_WORKLOADS["recovery_pool_host"], "mask": mask, "shapes": shapes,
+           "verified": bool(ok),
+           "rank": {n: {"us": v["rank_us"]} for n, v in shapes.items()}}
+    for v in shapes.values():
+        v.pop("rank_us")
+    return out
+
+
+def measure_set_diffs_host(torch, dist, ec, world, rank, args):
+    """The data side: the diffs of 65,536 SETs of 4098 B
+    (complete_nread, memcached.c:2676-2681: diff = new ^ ecmem[addr]), values pageable at
+    shuffled slots, old bytes at shuffled 16-B aligned addresses of a host ecmem registered
+    once (read in place by the kernel), one cec_region_multiply_batch (a prepared job list)
+    per step.  CPU beside it: memcpy + XOR per SET, 1 thread; its diffs check the batch's."""
+    import numpy as np
+    from oracle import pyoracle
+
+    N, size = 65536, 4098
+    stride = (size + 15) & ~15
+    rng = np.random.default_rng(0xC0C7000C + rank)
+    ecmem = host_array(N * stride, 0xC0C7000D + rank)
+    values = host_array(N * stride, 0xC0C7000E + rank)
+    diffs = host_array(N * stride)
+    diffs[:] = 0
+    vslot = rng.permutation(N).astype(np.uint64) * np.uint64(stride)
+    addrs = rng.permutation(N).astype(np.uint64) * np.uint64(stride)
+    doffs = np.arange(N, dtype=np.uint64) * np.uint64(stride)
+    vb, db, eb = values.ctypes.data, diffs.ctypes.data, ecmem.ctypes.data
+    jobs = ec.region_jobs([(vb + int(vslot[i]), db + int(doffs[i]), eb + int(addrs[i]), size, 1, 1)
+                           for i in range(N)])
+    ec.host_register(ecmem)
+    try:
+        for _ in range(max(1, args.warmup)):
+            ec.region_multiply_batch(jobs)
+        if dist_on(dist):
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            launches, rounds = ec.region_multiply_batch(jobs)  # synchronous
+        el = time.perf_counter() - t0
+        stats = ec.batch_stats()
+        if dist_on(dist):
+            dist.barrier()
+    finally:
+        ec.host_unregister(ecmem)
+    cpu = host_array(N * stride)
+    cpu[:] = 0
+    lens = np.full(N, size, np.uint32)
+    ts = [pyoracle.bench_set_diffs(values, vslot, ecmem, addrs, lens, cpu, doffs) for _ in range(3)]
+    ok = bool(np.array_equal(diffs, cpu))
+    own = el
+    el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
+    gib = N * size / 2**30
+    out = {"value": round(gib * world * args.steps / el, 2), "unit": "GiB/s of values",
+           "ms_per_step": round(el * 1e3 / args.steps, 3), "us_per_set": round(el * 1e6 / args.steps / N, 4),
+           "workload": EXTRA_WORKLOADS["set_diffs_host"],
+           "last_batch": {"launches": launches, "rounds": rounds, "in_place_launches": stats["in_place_launches"],
+                          "plan_us": round(stats["plan_us"]), "pack_us": round(stats["pack_us"]),
+                          "gpu_wait_us": round(stats["gpu_us"]), "unpack_us": round(stats["unpack_us"])},
+           "verified": ok and bad == 0.0,
+           "rank": {"ms_per_step": round(own * 1e3 / args.steps, 3), "verified": ok}}
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = _cpu_entry(gib, ts, "the reference's SET-diff code over the same 65,536 SETs "
+                                                  "(memcpy, then XOR with the old bytes), 1 thread, median of 3")
+        out["gpu_over_cpu"] = round(out["value"] / out["cpu_baseline"]["value"], 2)
+    return out
+
+
+SERVER_MEASURE = {"drain_host_ecmem": measure_drain_host, "recovery_pool_host": measure_recovery_pool_host,
+                  "set_diffs_host": measure_set_diffs_host}
+
+
 def run_device(args):
     torch, dist, ec, world, rank = setup(args.dist_backend)
 
@@ -898,6 +1155,9 @@ def run_device(args):
             continue
         if w == "rs32_1m_recovery":
             also[w] = measure_recovery_decode(torch, dist, ec, world, rank, args)
+            continue
+        if w in SERVER_MEASURE:
+            also[w] = SERVER_MEASURE[w](torch, dist, ec, world, rank, args)
             continue
         if w == "rs32_4k_lds":
             ec.set_engine(ec.CEC_ENGINE_LDS)

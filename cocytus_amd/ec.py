@@ -168,6 +168,7 @@ _SIGS = {
     "cec_recovery_pool_destroy": ([_vp], _i),
     "cec_recovery_pool_begin": ([_vp, _u32, _i, _i], _i),
     "cec_recovery_pool_add_peer": ([_vp, _i, _i, _vp], _i),
+    "cec_recovery_pool_add_peers": ([_vp, _ip, _ip, _pp, _i], _i),
     "cec_recovery_pool_flush": ([_vp, _vp], _i),
     "cec_recovery_pool_flush_solve": ([_vp, _pp, _vp], _i),
     "cec_recovery_pool_solved": ([_vp, _i], _i),
@@ -674,6 +675,12 @@ class RecoveryPool:
         ptr = units if isinstance(units, int) else _host_or_dev(units)
         _check(lib().cec_recovery_pool_add_peer(self._h, rid, peer_lid, ptr))
 
+    def add_peers(self, ids, peer_lids=None, units=None) -> None:
+        """n replies in one call (cec_recovery_pool_add_peers): lists of request ids, data
+        peer lids and buffers / staging addresses, or one pool_replies() tuple built ahead."""
+        ia, pa, ua, n = ids if peer_lids is None else pool_replies(ids, peer_lids, units)
+        _check(lib().cec_recovery_pool_add_peers(self._h, ia, pa, ua, n))
+
     def staging(self, rid: int, peer_lid: int):
         """(address, numpy uint8 view) where peer_lid's reply for rid may be received in place."""
         import numpy as np
@@ -783,6 +790,13 @@ class RecoveryPool:
             pass
 
 
+def pool_replies(ids, peer_lids, units) -> tuple:
+    """The argument arrays of cec_recovery_pool_add_peers (units: buffers or addresses)."""
+    n = len(ids)
+    ua = (ctypes.c_void_p * max(n, 1))(*[u if isinstance(u, int) else _host_or_dev(u) for u in units])
+    return _int_array(ids), _int_array(peer_lids), ua, n
+
+
 class Event:
     def __init__(self):
         self._e = ctypes.c_void_p()
@@ -818,14 +832,22 @@ def galois_w08_region_multiply(region, multby: int, nbytes: int, r2, add: int) -
     lib().galois_w08_region_multiply(_host_or_dev(region), multby, nbytes, _host_or_dev(r2), add)
 
 
-def region_multiply_batch(jobs, stream=None) -> tuple[int, int]:
-    """cec_region_multiply_batch over host buffers.  jobs: (src, dst, base, len, multby,
-    add) with src / dst / base as host addresses (int), numpy arrays, bytearrays or None.
-    Returns (kernel launches, staging rounds) of the call."""
+def region_jobs(jobs) -> ctypes.Array:
+    """A cec_region_job array of (src, dst, base, len, multby, add) tuples, built once (a
+    batch re-run with the same jobs passes the array itself)."""
     arr = (RegionJob * len(jobs))()
     for i, (src, dst, base, n, c, add) in enumerate(jobs):
         arr[i] = RegionJob(_host_or_dev(src), _host_or_dev(dst), _host_or_dev(base), n, c, add)
-    _check(lib().cec_region_multiply_batch(arr, len(jobs), _stream(stream)))
+    return arr
+
+
+def region_multiply_batch(jobs, stream=None) -> tuple[int, int]:
+    """cec_region_multiply_batch over host buffers.  jobs: (src, dst, base, len, multby,
+    add) with src / dst / base as host addresses (int), numpy arrays, bytearrays or None
+    (or a region_jobs() array).
+    Returns (kernel launches, staging rounds) of the call."""
+    arr = jobs if isinstance(jobs, ctypes.Array) else region_jobs(jobs)
+    _check(lib().cec_region_multiply_batch(arr, len(arr), _stream(stream)))
     st = batch_stats()
     return st["launches"], st["rounds"]
 

@@ -368,6 +368,11 @@ int cec_recovery_pool_begin(cec_recovery_pool *pool, uint32_t mask, int unit_beg
 /* complete_recovery_nread: data peer peer_lid's raw units of request id (host or
  * device).  Queued, not yet folded. */
 int cec_recovery_pool_add_peer(cec_recovery_pool *pool, int id, int peer_lid, const void *units);
+/* The same for n replies of an event-loop pass (reply i: request ids[i], data peer
+ * peer_lids[i], bytes units[i]), in one call: every reply is checked as add_peer checks it
+ * (and no (request, peer) pair twice) before any is queued; CEC_EINVAL queues nothing. */
+int cec_recovery_pool_add_peers(cec_recovery_pool *pool, const int *ids, const int *peer_lids,
+                                const void *const *units, int n);
 /* Where peer peer_lid's reply for request id may be received in place (pinned, mapped;
  * *len bytes): add_peer on this pointer copies nothing. */
 uint8_t *cec_recovery_pool_staging(cec_recovery_pool *pool, int id, int peer_lid, size_t *len);

@@ -259,3 +259,60 @@ double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+static double secs(struct timespec a, struct timespec b)
+{
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}
+
+double ref_bench_set_diffs(const uint8_t *values, const uint64_t *voffs, const uint8_t *ecmem,
+                           const uint64_t *addrs, const uint32_t *lens, int n, uint8_t *diffs,
+                           const uint64_t *doffs)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int i = 0; i < n; ++i) { /* memcached.c:2678-2681 */
+        memcpy(diffs + doffs[i], values + voffs[i], lens[i]);
+        ref_region_multiply_simd(ecmem + addrs[i], 1, (long)lens[i], diffs + doffs[i]);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return secs(t0, t1);
+}
+
+double ref_bench_recover_requests(const uint8_t *ecmem, const int *starts, int nreq, int units,
+                                  const uint8_t *const *replies, int npeers, const int *coefs, int inv,
+                                  uint8_t *const *outs)
+{
+    const size_t U = 4096, nbuf = (size_t)units * U;
+    uint8_t **unit = (uint8_t **)calloc((size_t)nreq * (size_t)units, sizeof(uint8_t *));
+    uint8_t **data = (uint8_t **)calloc((size_t)nreq, sizeof(uint8_t *));
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int q = 0; q < nreq; ++q)
+        for (int p = 0; p < npeers; ++p)
+            for (int i = 0; i < units; ++i) { /* recovery.c:72-94 */
+                uint8_t **u = &unit[(size_t)q * (size_t)units + (size_t)i];
+                if (!*u) { /* first touch: malloc(UNITSIZE) + memcpy of the parity unit */
+                    *u = (uint8_t *)malloc(U);
+                    memcpy(*u, ecmem + ((size_t)starts[q] + (size_t)i) * U, U);
+                }
+                ref_region_multiply_simd(replies[(size_t)q * (size_t)npeers + (size_t)p] + (size_t)i * U, coefs[p],
+                                         (long)U, *u);
+            }
+    for (int q = 0; q < nreq; ++q) { /* memcached.c:7853-7922, one lost shard */
+        uint8_t *buf = (uint8_t *)malloc(nbuf);
+        for (int i = 0; i < units; ++i) memcpy(buf + (size_t)i * U, unit[(size_t)q * (size_t)units + (size_t)i], U);
+        data[q] = (uint8_t *)calloc(1, nbuf);
+        ref_region_multiply_simd(buf, inv, (long)nbuf, data[q]);
+        free(buf);
+    }
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    for (int q = 0; q < nreq; ++q) {
+        memcpy(outs[q], data[q], nbuf);
+        free(data[q]);
+    }
+    for (size_t x = 0; x < (size_t)nreq * (size_t)units; ++x) free(unit[x]);
+    free(unit);
+    free(data);
+    return secs(t0, t1);
+}

@@ -144,6 +144,26 @@ double ref_bench_apply(const uint8_t *stage, const uint64_t *soffs, const uint64
 double ref_bench_recover(const uint8_t *parity, const uint8_t *const *peers, const int *coefs,
                          int npeers, int inv, long nbuf, uint8_t *residual, uint8_t *out);
 
+/* A data process's SET diffs as the reference computes them (one thread, complete_nread,
+ * memcached.c:2676-2681): per SET, diff = value (memcpy), then diff ^= 1 * ecmem[addr]
+ * (galois_w08_region_multiply).  Value i at values + voffs[i], diff i at diffs + doffs[i].
+ * Seconds. */
+double ref_bench_set_diffs(const uint8_t *values, const uint64_t *voffs, const uint8_t *ecmem,
+                           const uint64_t *addrs, const uint32_t *lens, int n, uint8_t *diffs,
+                           const uint64_t *doffs);
+
+/* A parity leading the recovery of nreq requests of `units` 4 KiB units each (request q:
+ * units starts[q] .. starts[q] + units - 1 of ecmem), a single lost data shard, as the
+ * reference runs it on one thread: per reply (replies[q * npeers + p], coefficient
+ * coefs[p]) and per unit, recovery_recover_units (recovery.c:72-94: first touch mallocs the
+ * unit and copies the parity unit in, then the peer unit is region-multiplied in); then per
+ * request the bottom half (memcached.c:7853-7922: the units copied into one buffer, a
+ * calloc'd output, output ^= inv * buffer).  outs[q] (units * 4096 bytes) receive the
+ * rebuilt bytes after the clock stops.  Seconds. */
+double ref_bench_recover_requests(const uint8_t *ecmem, const int *starts, int nreq, int units,
+                                  const uint8_t *const *replies, int npeers, const int *coefs, int inv,
+                                  uint8_t *const *outs);
+
 #ifdef __cplusplus
 }
 #endif

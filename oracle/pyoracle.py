@@ -50,6 +50,10 @@ _SIGS = {
                          ctypes.c_void_p, _i, ctypes.c_void_p], ctypes.c_double),
     "ref_bench_recover": ([ctypes.c_void_p, _vpp, ctypes.c_void_p, _i, _i, _l, ctypes.c_void_p,
                            ctypes.c_void_p], ctypes.c_double),
+    "ref_bench_set_diffs": ([ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, _i, ctypes.c_void_p, ctypes.c_void_p], ctypes.c_double),
+    "ref_bench_recover_requests": ([ctypes.c_void_p, ctypes.c_void_p, _i, _i, _vpp, _i, ctypes.c_void_p, _i,
+                                    _vpp], ctypes.c_double),
 }
 
 _lib = None
@@ -237,6 +241,31 @@ def bench_recover(parity: np.ndarray, peers: list, coefs, inv: int) -> tuple[flo
     t = lib().ref_bench_recover(_p(parity), _arr(peers), cf.ctypes.data, len(peers), inv, n,
                                 _p(res), _p(out))
     return t, out
+
+
+def bench_set_diffs(values: np.ndarray, voffs, ecmem: np.ndarray, addrs, lens, diffs: np.ndarray,
+                    doffs) -> float:
+    """The reference's SET-diff loop (memcpy + XOR with the old bytes per SET, one thread)
+    over values / diffs packed at the given offsets; seconds."""
+    vo = np.ascontiguousarray(voffs, np.uint64)
+    ad = np.ascontiguousarray(addrs, np.uint64)
+    ln = np.ascontiguousarray(lens, np.uint32)
+    do = np.ascontiguousarray(doffs, np.uint64)
+    return lib().ref_bench_set_diffs(_p(values), vo.ctypes.data, _p(ecmem), ad.ctypes.data, ln.ctypes.data,
+                                     len(ln), _p(diffs), do.ctypes.data)
+
+
+def bench_recover_requests(ecmem: np.ndarray, starts, units: int, replies: list, npeers: int, coefs,
+                           inv: int) -> tuple[float, list]:
+    """The reference's recovery of len(starts) single-loss requests led by this parity
+    (per-unit folds with malloc'd units, then the bottom half), one thread; replies[q *
+    npeers + p].  Returns (seconds, [rebuilt bytes per request])."""
+    st = np.ascontiguousarray(starts, np.int32)
+    cf = np.ascontiguousarray(coefs, np.int32)
+    outs = [np.empty(units * 4096, np.uint8) for _ in range(len(st))]
+    t = lib().ref_bench_recover_requests(_p(ecmem), st.ctypes.data, len(st), units, _arr(replies), npeers,
+                                         cf.ctypes.data, inv, _arr(outs))
+    return t, outs
 
 
 def splitmix_bytes(seed: int, n: int) -> np.ndarray:

@@ -280,7 +280,8 @@ def test_share_layout_rebases_a_contiguous_split():
 
 def test_bench_arguments():
     """The driver's contract: no flags = N=1, the metric's workload, steps/warmup that
-    finish in minutes; the other device-resident configs ride along (--also)."""
+    finish in minutes; the other device-resident configs and the server placements (host
+    ecmem) ride along (--also)."""
     import bench
 
     a = bench.parse([])
@@ -288,7 +289,7 @@ def test_bench_arguments():
     assert 1 <= a.steps <= 100 and a.warmup >= 1
     assert set(a.also.split(",")) == {"rs32_4k_lds", "rs32_mixed", "rs32_1m", "rs42_64k",
                                       "rs32_1m_recovery", "rs32_diff_update", "rs32_diff_update_lds",
-                                      "rs32_e2e"}
+                                      "rs32_e2e", "drain_host_ecmem", "recovery_pool_host", "set_diffs_host"}
     assert not a.no_strong
     assert bench.parse(["--also="]).also == ""
     with pytest.raises(SystemExit):

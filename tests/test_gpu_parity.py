@@ -1777,6 +1777,54 @@ def test_recovery_pool_host_output_lifecycle(gpu, oracle):
         assert pool.output(a) is None
 
 
+def test_recovery_pool_add_peers_batch(gpu, oracle):
+    """cec_recovery_pool_add_peers (a pass's replies in one call): a batch with a bad reply
+    -- a peer twice for one request, a peer already applied, a parity lid, an ended request
+    -- is refused and queues nothing (the next flush folds nothing); the good batch, mixing
+    replies received in the pool's staging and copied from host buffers, rebuilds every
+    request's bytes in one flush_solve_host, as add_peer one by one does."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xADD5)
+    nunits = 64
+    data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+    p1 = to_dev(torch, oracle.encode(mat, k, m, data)[1])
+    mask = (1 << 4) | 0b101  # D1 lost, leader P1 (inverse 1/245)
+    starts = [0, 3, 10, 11, 30, 50]
+    with ec.RecoveryPool(k, m, mat, 4, p1, capacity_units=32) as pool:
+        ended = pool.begin(mask, 60, 60)
+        pool.end(ended)
+        rids = [pool.begin(mask, s, s + 1) for s in starts]  # two units each
+        pool.add_peer(rids[0], 0, data[0][0:2 * U].copy())  # D0 of the first already applied
+        ids, lids, bufs = [], [], []
+        for q, (rid, s) in enumerate(zip(rids, starts)):
+            for j in (0, 2):
+                if q == 0 and j == 0:
+                    continue
+                src = data[j][s * U:(s + 2) * U]
+                if (q + j) % 2:  # received in place
+                    addr, view = pool.staging(rid, j)
+                    view[:] = src
+                    bufs.append(addr)
+                else:
+                    bufs.append(src.copy())
+                ids.append(rid)
+                lids.append(j)
+        for bad in ((ids + [ids[1]], lids + [lids[1]], bufs + [bufs[1]]),  # a pair twice
+                    (ids + [rids[0]], lids + [0], bufs + [bufs[0]]),
+                    (ids + [rids[2]], lids + [3], bufs + [bufs[0]]),
+                    (ids + [ended], lids + [2], bufs + [bufs[0]])):
+            with pytest.raises(ec.CecError):
+                pool.add_peers(*bad)
+        assert all(not pool.complete(r) for r in rids)  # nothing of a refused batch queued
+        pool.add_peers(ids, lids, bufs)
+        assert pool.flush_solve_host() == len(rids)
+        for rid, s in zip(rids, starts):
+            assert np.array_equal(pool.output(rid), data[1][s * U:(s + 2) * U]), s
+        pool.add_peers([], [], [])  # an empty pass
+
+
 def test_recovery_pool_misuse_is_refused(gpu, oracle):
     """Stale and bad handles on the pool's calls (what a server bug would send): an ended or
     never-begun id, a repeated end, a reply or a solve for an ended request, a window with a

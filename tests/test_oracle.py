@@ -173,6 +173,38 @@ def test_simd_baseline_equals_scalar(oracle):
             assert np.array_equal(a, b)
 
 
+def test_cpu_baseline_server_loops(oracle):
+    """bench.py's 1-thread CPU legs of the server placements against the scalar oracle:
+    the SET-diff loop (memcached.c:2676-2681) gives value ^ old per SET; the recovery chain
+    (recovery.c:72-94 + memcached.c:7853-7922) gives inv * (parity ^ sum c_p * reply_p) per
+    request -- which is the lost shard's bytes when the parity is the code's."""
+    rng = np.random.default_rng(11)
+    n, size, stride = 50, 4098, 4112
+    ecmem = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    values = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    vo = rng.permutation(n).astype(np.uint64) * stride
+    ad = rng.permutation(n).astype(np.uint64) * stride
+    do = np.arange(n, dtype=np.uint64) * stride
+    diffs = np.zeros(n * stride, np.uint8)
+    assert oracle.bench_set_diffs(values, vo, ecmem, ad, np.full(n, size), diffs, do) >= 0
+    for i in range(n):
+        exp = oracle.set_diff(ecmem[int(ad[i]):int(ad[i]) + size].copy(), values[int(vo[i]):int(vo[i]) + size].copy())
+        assert np.array_equal(diffs[int(do[i]):int(do[i]) + size], exp)
+    k, m, U, self_lid, lost = 3, 2, 4096, 4, 1
+    mat = oracle.big_vandermonde(k + m, k)
+    nunits = 40
+    data = [rng.integers(0, 256, nunits * U, dtype=np.uint8) for _ in range(k)]
+    ecm = oracle.encode(mat, k, m, data)[1]  # this parity's arena: P1
+    inv = oracle.gf_div(1, mat[self_lid * k + lost])
+    for units, starts in ((8, [3]), (1, [0, 7, 39, 12])):
+        replies = [data[p][s * U:(s + units) * U].copy() for s in starts for p in (0, 2)]
+        t, outs = oracle.bench_recover_requests(ecm, starts, units, replies, 2,
+                                                [mat[self_lid * k + 0], mat[self_lid * k + 2]], inv)
+        assert t >= 0
+        for s, o in zip(starts, outs):
+            assert np.array_equal(o, data[lost][s * U:(s + units) * U]), (units, s)
+
+
 def test_known_matrices(oracle):
     # SURVEY.md §8c: restated answers of the survey's own (separate) restatement
     assert oracle.big_vandermonde(5, 3)[9:] == [1, 1, 1, 1, 245, 244]
