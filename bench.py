@@ -763,6 +763,20 @@ def measure_recovery_decode(torch, dist, ec, world, rank, args):
             "verified": all(c["verified"] for c in cases.values())}
 
 
+_PCIE = {}
+
+
+def pcie_floor(torch, h2d_bytes, d2h_bytes):
+    """The PCIe floor of a step that moves h2d_bytes host -> device and d2h_bytes back
+    (the two directions overlap): max over directions of bytes / this link's raw pinned
+    copy rate (measured once per process, outside every timed region).  Seconds, and the
+    rates."""
+    if not _PCIE:
+        _PCIE["h2d"], _PCIE["d2h"] = pcie_raw(torch)
+    return (max(h2d_bytes / (_PCIE["h2d"] * 1e9), d2h_bytes / (_PCIE["d2h"] * 1e9)),
+            {x: round(v, 1) for x, v in _PCIE.items()})
+
+
 def pcie_raw(torch, nbytes=256 << 20, reps=4):
     """Raw pinned H2D / D2H copy rates of this GPU's link (GB/s)."""
     x = torch.empty(nbytes, dtype=torch.uint8, pin_memory=True)
@@ -865,8 +879,8 @@ def measure_e2e(torch, dist, ec, world, rank, args):
     el = time.perf_counter() - t0
     if dist_on(dist):
         dist.barrier()
-    h2d, d2h = pcie_raw(torch)
-    floor_s = max(e.h2d_bytes / (h2d * 1e9), e.d2h_bytes / (d2h * 1e9))
+    floor_s, raw = pcie_floor(torch, e.h2d_bytes, e.d2h_bytes)
+    h2d, d2h = raw["h2d"], raw["d2h"]
     own = el
     el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
     out = {
@@ -963,8 +977,13 @@ def measure_drain_host(torch, dist, ec, world, rank, args):
     own = el
     el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
     gib = N * size / 2**30
+    # PCIe per step: the diffs up, the arena's bytes read and written back (read-modify-write
+    # of the registered host ecmem by the kernel)
+    floor, raw = pcie_floor(torch, 2 * N * size, N * size)
     out = {"value": round(gib * world * args.steps / el, 2), "unit": "GiB/s of diffs",
            "ms_per_step": round(el * 1e3 / args.steps, 3), "us_per_diff": round(el * 1e6 / args.steps / N, 4),
+           "pcie_bound_frac": round(floor / (own / args.steps), 4), "pcie_GBps_raw": raw,
+           "pcie_bytes_per_step": {"h2d": 2 * N * size, "d2h": N * size},
            "workload": EXTRA_WORKLOADS["drain_host_ecmem"], "launches_per_apply": launches,
            "verified": ok and bad == 0.0,
            "rank": {"ms_per_step": round(own * 1e3 / args.steps, 3), "verified": ok}}
@@ -1040,9 +1059,13 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
             g_med, c_med = statistics.median(gpu_t), statistics.median(cpu_t)
             g_max = max_over_ranks([g_med], dist)[0]
             gib = 3 * nreq * units * U / 2**30  # two replies folded + the bytes rebuilt
+            # PCIe per pass: the parity units and both replies read in place, the rebuilt bytes
+            # written to the mapped output
+            floor, _ = pcie_floor(torch, 3 * nreq * units * U, nreq * units * U)
             shapes[name] = {"requests": nreq, "units_per_request": units, "reps": reps,
                             "us": round(g_max * 1e6, 1), "value": round(gib * world / g_max, 3),
                             "unit": "GiB/s (replies folded + bytes rebuilt)",
+                            "pcie_floor_us": round(floor * 1e6, 1), "pcie_bound_frac": round(floor / g_med, 4),
                             "rank_us": round(g_med * 1e6, 1)}
             if world == 1 and not args.no_cpu_baseline:
                 shapes[name]["cpu_baseline"] = _cpu_entry(
@@ -1056,6 +1079,7 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
     ok, = [x == 0.0 for x in max_over_ranks([0.0 if ok else 1.0], dist)]
     out = {"value": shapes["range_1MiB"]["value"], "unit": shapes["range_1MiB"]["unit"] + ", 1 MiB range",
            "workload": EXTRA_WORKLOADS["recovery_pool_host"], "mask": mask, "shapes": shapes,
+           "pcie_GBps_raw": {x: round(v, 1) for x, v in _PCIE.items()},
            "verified": bool(ok),
            "rank": {n: {"us": v["rank_us"]} for n, v in shapes.items()}}
     for v in shapes.values():
@@ -1108,8 +1132,12 @@ def measure_set_diffs_host(torch, dist, ec, world, rank, args):
     own = el
     el, bad = max_over_ranks([el, 0.0 if ok else 1.0], dist)
     gib = N * size / 2**30
+    # PCIe per step: the values up (staged) and the old bytes read in place; the diffs back
+    floor, raw = pcie_floor(torch, 2 * N * size, N * size)
     out = {"value": round(gib * world * args.steps / el, 2), "unit": "GiB/s of values",
            "ms_per_step": round(el * 1e3 / args.steps, 3), "us_per_set": round(el * 1e6 / args.steps / N, 4),
+           "pcie_bound_frac": round(floor / (own / args.steps), 4), "pcie_GBps_raw": raw,
+           "pcie_bytes_per_step": {"h2d": 2 * N * size, "d2h": N * size},
            "workload": EXTRA_WORKLOADS["set_diffs_host"],
            "last_batch": {"launches": launches, "rounds": rounds, "in_place_launches": stats["in_place_launches"],
                           "plan_us": round(stats["plan_us"]), "pack_us": round(stats["pack_us"]),

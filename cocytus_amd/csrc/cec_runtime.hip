@@ -594,9 +594,22 @@ static int launch_combine(int dev, const Streams &st, const uint8_t *tables, siz
     return CEC_OK;
 }
 
+// Test hook (cec_internal_fail_launch): the calling thread's next `after` launches run, the
+// one after them is refused as a HIP failure, then the hook disarms.  -1: off.
+static thread_local int t_fail_after = -1;
+CEC_API int cec_internal_fail_launch(int after) {
+    t_fail_after = after < 0 ? -1 : after;
+    return CEC_OK;
+}
+
 static int run_combine(int dev, const Streams &st, const std::vector<Pattern> &pats,
                        const std::vector<uint8_t> &rows, const cec_plan *plan,
                        uint64_t implicit_len, hipStream_t stream, const std::vector<char> *used, int engine) {
+    if (t_fail_after == 0) {
+        t_fail_after = -1;
+        return fail(CEC_EHIP, "injected launch failure (cec_internal_fail_launch)");
+    }
+    if (t_fail_after > 0) --t_fail_after;
     uint64_t n_tiles;
     if (plan) {
         if (plan->device != dev)

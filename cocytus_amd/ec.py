@@ -122,6 +122,7 @@ _SIGS = {
     "cec_last_engine": ([], _i),
     "cec_internal_check_launch_layout": ([_i, _ip, _i, _ip, _i, _pp, _i], _i),
     "cec_internal_store_policy": ([ctypes.POINTER(ctypes.c_uint64)], _i),
+    "cec_internal_fail_launch": ([_i], _i),
     "cec_plan_release_stream": ([_vp, _vp], _i),
     "cec_plan_tracked_streams": ([_vp], _i),
     "cec_drainer_release_stream": ([_vp, _vp], _i),
@@ -369,6 +370,12 @@ def store_policy() -> tuple[str, int]:
     v = ctypes.c_uint64()
     p = lib().cec_internal_store_policy(ctypes.byref(v))
     return {0: "auto", 1: "nt", 2: "wt"}[p], int(v.value)
+
+
+def fail_launch(after: int) -> None:
+    """cec_internal_fail_launch (test hook): the thread's launch number `after` (0-based)
+    fails with CEC_EHIP; -1 disarms."""
+    _check(lib().cec_internal_fail_launch(after))
 
 
 def set_waves_per_cu(waves: int) -> None:

@@ -459,7 +459,7 @@ typedef struct cec_sync_record {
 } cec_sync_record;
 int cec_last_sync(cec_sync_record *out);
 
-/* ---- test hooks (host only, launch nothing; not for servers) ----
+/* ---- test hooks (host only, launch nothing themselves; not for servers) ----
  * cec_internal_check_launch_layout: the launch-time check every op's launch runs, on one
  * pattern reading in_slots and writing out_slots, against the kernel argument block built
  * from bases[0..n_bases) -- the two-slot block of the narrow 1 x 1 kernels (narrow != 0)
@@ -471,6 +471,10 @@ int cec_last_sync(cec_sync_record *out);
 int cec_internal_check_launch_layout(int narrow, const int *in_slots, int n_in, const int *out_slots,
                                      int n_out, const void *const *bases, int n_bases);
 int cec_internal_store_policy(uint64_t *wt_max_bytes);
+/* cec_internal_fail_launch: fault injection for the error paths (tests only) -- the calling
+ * thread's next `after` kernel launches run and the one after them fails as a HIP error
+ * would (CEC_EHIP, nothing launched); then the hook disarms.  after < 0 disarms it. */
+int cec_internal_fail_launch(int after);
 
 /* ---- stream / event helpers, so C and ctypes callers need no HIP header ----
  * Events are for timing: recorded without the system-scope fence, so waiting on one

@@ -549,3 +549,89 @@ def test_release_stream_refused_while_capturing(gpu, oracle):
     plan.release_stream(s)
     assert plan.tracked_streams == listed - 1
     plan.destroy()
+
+
+@pytest.mark.parametrize("path", ["drain_small", "drain_pack", "host_batch", "pool_fold_updates"])
+def test_failed_later_wave_leaves_nothing_in_flight(gpu, oracle, path):
+    """A launch that fails after earlier waves of the same call ran (fault injection:
+    cec_internal_fail_launch(1) -- the second launch of the call fails as a HIP error
+    would): the call returns CEC_EHIP only after the first wave has completed, so nothing of
+    it still reads the object's staging when the next call overwrites it.  A
+    window of distinct 4 KiB updates plus one exact duplicate of the first takes two waves:
+    the first wave holds every distinct update once, whichever of the twin pair it took.
+    Checked: the registered host arena holds exactly the first wave's bytes on return (read
+    without a device sync), the host batch wrote no destination, the pool's residual holds
+    the first wave's folds; then the whole window again gives the reference's bytes."""
+    torch, ec = gpu
+    k, m, U = 3, 2, 4096
+    mat = ec.coding_matrix(k, m)
+    rng = np.random.default_rng(0xFA11 + len(path))
+    n = 24 if path in ("drain_small", "pool_fold_updates") else 400  # 400 x 4 KiB: the pack path
+    lid_self, src = k, 1
+    c = mat[lid_self * k + src]
+    ups = [(rng.integers(0, 256, U, dtype=np.uint8), 2 * i * U, src) for i in range(n)]
+    ups.append((ups[0][0].copy(), ups[0][1], src))  # the twin: a second wave
+    once = np.zeros(2 * n * U + U, np.uint8)  # c * every distinct update, once
+    for buf, addr, _ in ups[:n]:
+        oracle.region_multiply(buf, c, once[addr:addr + U], 1)
+    try:
+        if path.startswith("drain"):
+            arena = rng.integers(0, 256, once.size, dtype=np.uint8)
+            before = arena.copy()
+            alias = ec.host_register(arena)
+            try:
+                with ec.Drainer(k, m, mat, lid_self, staging_bytes=8 << 20) as d:
+                    ec.fail_launch(1)
+                    with pytest.raises(ec.CecError) as e:
+                        d.apply(ups, alias)
+                    assert e.value.code == ec.CEC_EHIP
+                    assert np.array_equal(arena, before ^ once)  # wave 0 complete on return
+                    d.apply(ups, alias)  # the whole window: the twin pair cancels
+                    exp = before ^ once
+                    oracle.region_multiply(ups[0][0], c, exp[0:U], 1)
+                    assert np.array_equal(arena, exp)
+            finally:
+                ec.host_unregister(arena)
+        elif path == "host_batch":
+            dst = rng.integers(0, 256, once.size, dtype=np.uint8)
+            before = dst.copy()
+            jobs = [(buf, dst.ctypes.data + addr, None, U, c, 1) for buf, addr, _ in ups]
+            ec.fail_launch(1)
+            with pytest.raises(ec.CecError) as e:
+                ec.region_multiply_batch(jobs)
+            assert e.value.code == ec.CEC_EHIP
+            assert np.array_equal(dst, before)  # nothing unpacked: no destination written
+            assert ec.region_multiply_batch(jobs)[0] == 2  # two waves
+            exp = before ^ once
+            oracle.region_multiply(ups[0][0], c, exp[0:U], 1)
+            assert np.array_equal(dst, exp)
+        else:
+            data = [rng.integers(0, 256, once.size, dtype=np.uint8) for _ in range(k)]
+            par = to_dev_np(torch, oracle.encode(mat, k, m, data)[0])
+            nunits = once.size // U
+            mask = (1 << lid_self) | 0b110  # D0 lost, leader P0; D1 has not replied yet
+            with ec.RecoveryPool(k, m, mat, lid_self, par, capacity_units=nunits) as pool:
+                rid = pool.begin(mask, 0, nunits - 1)
+                pool.add_peer(rid, 2, data[2].copy())
+                pool.flush()
+                res0 = np.empty(once.size, np.uint8)
+                pool.residual(rid, res0)
+                ec.fail_launch(1)
+                with pytest.raises(ec.CecError) as e:
+                    pool.fold_updates(ups)
+                assert e.value.code == ec.CEC_EHIP
+                res1 = np.empty(once.size, np.uint8)
+                pool.residual(rid, res1)
+                assert np.array_equal(res1, res0 ^ once)
+                pool.fold_updates(ups)
+                res2 = np.empty(once.size, np.uint8)
+                pool.residual(rid, res2)
+                exp = res0 ^ once ^ once
+                oracle.region_multiply(ups[0][0], c, exp[0:U], 1)
+                assert np.array_equal(res2, exp)
+    finally:
+        ec.fail_launch(-1)
+
+
+def to_dev_np(torch, a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()

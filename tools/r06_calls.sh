@@ -5,6 +5,7 @@
 #   f  the final tree as the driver runs it: smoke, the whole GPU suite, the default line
 #   g  rocprofv3 --kernel-trace --stats of the driver's exact command (python bench.py, no
 #      flags) with its line, for tools/trace_check.py (encode and decode dispatches)
+#   z  f, then g
 set -o pipefail
 case "$1" in
 a)
@@ -28,6 +29,10 @@ g)
     cd /tmp && export TMPDIR=/tmp
     timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof_r06_default" -o run \
         --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" > $out/bench_default.jsonl 2> $out/bench_default.err
+    ;;
+z)  # f then g in one call (one box acquisition): the final tree's evidence set
+    bash tools/r06_calls.sh f || exit $?
+    bash tools/r06_calls.sh g || exit $?
     ;;
 *) echo "unknown case $1"; exit 9 ;;
 esac
