@@ -586,8 +586,8 @@ def test_failed_later_wave_leaves_nothing_in_flight(gpu, oracle, path):
                         d.apply(ups, alias)
                     assert e.value.code == ec.CEC_EHIP
                     assert np.array_equal(arena, before ^ once)  # wave 0 complete on return
-                    d.apply(ups, alias)  # the whole window: the twin pair cancels
-                    exp = before ^ once
+                    d.apply(ups, alias)  # the whole window again: every update twice
+                    exp = before.copy()   # but the first (three times in all)
                     oracle.region_multiply(ups[0][0], c, exp[0:U], 1)
                     assert np.array_equal(arena, exp)
             finally:
