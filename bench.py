@@ -1028,7 +1028,7 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
         for name, units, starts in (("range_1MiB", 256, [100]), ("idle_85", 1, starts85)):
             nreq = len(starts)
             replies = [host_array(units * U, 0xC0C70100 + 7 * rank + x) for x in range(2 * nreq)]
-            gpu_t, cpu_t = [], []
+            gpu_t, cpu_t, add_t = [], [], []
             with ec.RecoveryPool(k, m, mat, SELF, alias, capacity_units=nreq * units) as pool:
                 for rep in range(reps + 1):  # rep 0: warm-up
                     first = [s + rep * walk for s in starts]
@@ -1046,6 +1046,7 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
                         dist.barrier()
                     t0 = time.perf_counter()
                     pool.add_peers(arrs)
+                    tm = time.perf_counter()
                     solved = pool.flush_solve_host()
                     t1 = time.perf_counter()
                     got = [pool.output(rid).copy() for rid in rids]  # fill_completed_recovered_data
@@ -1055,6 +1056,7 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
                     ok &= solved == nreq and all(np.array_equal(g, e) for g, e in zip(got, exp))
                     if rep:
                         gpu_t.append(t1 - t0)
+                        add_t.append(tm - t0)
                         cpu_t.append(tc)
             g_med, c_med = statistics.median(gpu_t), statistics.median(cpu_t)
             g_max = max_over_ranks([g_med], dist)[0]
@@ -1066,6 +1068,7 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
                             "us": round(g_max * 1e6, 1), "value": round(gib * world / g_max, 3),
                             "unit": "GiB/s (replies folded + bytes rebuilt)",
                             "pcie_floor_us": round(floor * 1e6, 1), "pcie_bound_frac": round(floor / g_med, 4),
+                            "add_peers_us": round(statistics.median(add_t) * 1e6, 1),  # the rest: the flush
                             "rank_us": round(g_med * 1e6, 1)}
             if world == 1 and not args.no_cpu_baseline:
                 shapes[name]["cpu_baseline"] = _cpu_entry(
