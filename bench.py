@@ -1049,11 +1049,12 @@ def measure_recovery_pool_host(torch, dist, ec, world, rank, args):
                     tm = time.perf_counter()
                     solved = pool.flush_solve_host()
                     t1 = time.perf_counter()
-                    got = [pool.output(rid).copy() for rid in rids]  # fill_completed_recovered_data
+                    got = [pool.output(rid) for rid in rids]  # fill_completed_recovered_data
+                    got = [None if g is None else g.copy() for g in got]  # (None: not solved)
                     for rid in rids:
                         pool.end(rid)
                     tc, exp = pyoracle.bench_recover_requests(ecmem, first, units, replies, 2, coefs, inv)
-                    ok &= solved == nreq and all(np.array_equal(g, e) for g, e in zip(got, exp))
+                    ok &= solved == nreq and all(g is not None and np.array_equal(g, e) for g, e in zip(got, exp))
                     if rep:
                         gpu_t.append(t1 - t0)
                         add_t.append(tm - t0)
