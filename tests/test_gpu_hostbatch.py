@@ -284,3 +284,28 @@ def test_batch_bases_in_place_from_a_registered_region(gpu, oracle):
     # unregistered again: staged
     _run(ec, heap, [((5 << 20), (8 << 20), 0, 4096, 3, 1)])
     assert ec.batch_stats()["in_place_launches"] == 0
+
+
+def test_batch_pipelined_rounds_in_place_odd_sizes(gpu, oracle):
+    """A batch above 4 MiB runs as double-buffered rounds; with 4098-B SETs the staging half's
+    size is no multiple of 16 unless rounded: every round -- the odd ones in the
+    second half included -- must read its bases in place and leave the sequential chain's
+    bytes.  2,000 SET diffs (memcached.c:2676-2681: diff = old ^ 1 * value), old bytes in a
+    registered arena at shuffled 16-B aligned addresses."""
+    torch, ec = gpu
+    rng = np.random.default_rng(4098)
+    n_sets, size, stride = 2000, 4098, 4112
+    heap = rng.integers(0, 256, 48 << 20, dtype=np.uint8)
+    arena = heap[:n_sets * stride]                  # the registered ecmem
+    vbase, dbase = 16 << 20, 32 << 20
+    slots = rng.permutation(n_sets)
+    jobs = [(vbase + i * stride, dbase + i * stride, int(slots[i]) * stride, size, 1, 1) for i in range(n_sets)]
+    want = _model(oracle, heap, jobs)
+    ec.host_register(arena)
+    try:
+        launches, rounds = _run(ec, heap, jobs)
+        st = ec.batch_stats()
+    finally:
+        ec.host_unregister(arena)
+    assert np.array_equal(heap, want)
+    assert rounds >= 4 and st["in_place_launches"] == launches == rounds
